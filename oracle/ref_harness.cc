@@ -1,0 +1,181 @@
+// TEST INFRASTRUCTURE ONLY — a driver that links the UNMODIFIED reference objects built from
+// /root/reference by oracle/Makefile (into oracle/_ref/) and calls the reference's own functions,
+// so the golden vectors under tests/golden/ are produced by the reference itself.
+//
+// Reference entry points called (file:line in /root/reference):
+//   Hash::LSH::generateHashTable        hash/lshash.cc:36
+//   Hash::LSH::random_projection        hash/lshash.cc:53
+//   p_cluster                           function/cluster.cc:56
+//   Cluster                             function/cluster.cc:181
+//   Core::Distance::cosine              function/distance.cc:27
+//   Core::AB::SetConsensus              function/funcAB.cc:49
+//   Utility::IOMat::ReadClusterAll      io/ioMatrix.cc:48
+//   Utility::IOMat::SaveResult / SaveBinary   io/ioMatrix.cc:265 / :322
+//   Utility::IOMat::convertHTMat        io/ioMatrix.cc:353
+//
+// Run with OMP_THREAD_LIMIT=1 (T=1 semantics) and KLSH_SEED=<seed> (ref_seed.cc).
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "function/cluster.h"
+#include "io/ioMatrix.h"
+
+using namespace std;
+
+static vector<float> read_f32(const char* path, size_t count) {
+  vector<float> v(count);
+  FILE* f = fopen(path, "rb");
+  if (!f) { perror(path); exit(2); }
+  if (count && fread(v.data(), 4, count, f) != count) { fprintf(stderr, "short read %s\n", path); exit(2); }
+  fclose(f);
+  return v;
+}
+
+static void write_bytes(const char* path, const void* p, size_t n) {
+  FILE* f = fopen(path, "wb");
+  if (!f) { perror(path); exit(2); }
+  if (n) fwrite(p, 1, n, f);
+  fclose(f);
+}
+
+static vector<Abundance*> rows_to_abundance(const vector<float>& x, size_t n, int d) {
+  vector<Abundance*> v;
+  v.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    Abundance* a = new Abundance();
+    a->_values.assign(x.begin() + i * d, x.begin() + (i + 1) * d);
+    a->_ids.push_back(i);
+    v.push_back(a);
+  }
+  return v;
+}
+
+static void save(vector<Abundance*>* v, const string& prefix) {
+  // The reference's own writers, ignore_small = 0 (every cluster).
+  IOMat::SaveResult(v, prefix + ".clust", true, 0, false);
+  IOMat::SaveBinary(v, prefix, true, 0, false);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    fprintf(stderr,
+            "usage:\n"
+            "  ref_harness rng H D                          (hex floats of generateHashTable(H,D))\n"
+            "  ref_harness keys ROWS N D H OUT              (uint32 keys via random_projection)\n"
+            "  ref_harness pcluster ROWS N D THR OUTPREFIX  (one bucket through p_cluster)\n"
+            "  ref_harness cosine ROWS N D OUT              (float cosine distance for pairs (i, i+1))\n"
+            "  ref_harness consensus ROWS D CA CB OUT       (SetConsensus of row0 (CA ids) and row1 (CB ids))\n"
+            "  ref_harness cluster ROWS N D MINSIM I BTHR OUTPREFIX\n"
+            "  ref_harness cluster_from BINPREFIX D MINSIM I BTHR OUTPREFIX   (input via ReadClusterAll)\n"
+            "  ref_harness convert COUNTS N D VKMERS OUTPREFIX  (uint16 sample-major counts -> convertHTMat)\n");
+    return 1;
+  }
+  const string cmd = argv[1];
+  if (cmd == "rng") {
+    const int h = atoi(argv[2]), d = atoi(argv[3]);
+    hashTable t = LSH::generateHashTable(h, d);
+    for (int j = 0; j < h; ++j) {
+      for (int i = 0; i < d; ++i) {
+        uint32_t b;
+        memcpy(&b, &t[j][i], 4);
+        printf("%s%08x", i ? " " : "", b);
+      }
+      printf("\n");
+    }
+    return 0;
+  }
+  if (cmd == "keys") {
+    const size_t n = strtoull(argv[3], nullptr, 10);
+    const int d = atoi(argv[4]), h = atoi(argv[5]);
+    vector<float> x = read_f32(argv[2], n * d);
+    hashTable t = LSH::generateHashTable(h, d);
+    vector<uint32_t> keys(n);
+    for (size_t i = 0; i < n; ++i) {
+      vector<float> row(x.begin() + i * d, x.begin() + (i + 1) * d);
+      keys[i] = (uint32_t)LSH::random_projection(row, t);
+    }
+    write_bytes(argv[6], keys.data(), n * 4);
+    return 0;
+  }
+  if (cmd == "pcluster") {
+    const size_t n = strtoull(argv[3], nullptr, 10);
+    const int d = atoi(argv[4]);
+    const float thr = (float)atof(argv[5]);
+    vector<float> x = read_f32(argv[2], n * d);
+    vector<Abundance*> bucket = rows_to_abundance(x, n, d);
+    vector<Abundance*> out;
+    p_cluster(&out, &bucket, thr);
+    save(&out, argv[6]);
+    return 0;
+  }
+  if (cmd == "cosine") {
+    const size_t n = strtoull(argv[3], nullptr, 10);
+    const int d = atoi(argv[4]);
+    vector<float> x = read_f32(argv[2], n * d);
+    vector<float> out;
+    for (size_t i = 0; i + 1 < n; ++i) {
+      vector<float> a(x.begin() + i * d, x.begin() + (i + 1) * d);
+      vector<float> b(x.begin() + (i + 1) * d, x.begin() + (i + 2) * d);
+      out.push_back(Distance::cosine(a, b));
+    }
+    write_bytes(argv[5], out.data(), out.size() * 4);
+    return 0;
+  }
+  if (cmd == "consensus") {
+    const int d = atoi(argv[3]);
+    const int ca = atoi(argv[4]), cb = atoi(argv[5]);
+    vector<float> x = read_f32(argv[2], 2 * (size_t)d);
+    Abundance a, b, c;
+    a._values.assign(x.begin(), x.begin() + d);
+    b._values.assign(x.begin() + d, x.begin() + 2 * d);
+    for (int i = 0; i < ca; ++i) a._ids.push_back(i);
+    for (int i = 0; i < cb; ++i) b._ids.push_back(1000000 + i);
+    AB::SetConsensus(&c, a, b);
+    write_bytes(argv[6], c._values.data(), (size_t)d * 4);
+    return 0;
+  }
+  if (cmd == "cluster" || cmd == "cluster_from") {
+    vector<Abundance*> v;
+    int argi;
+    int d;
+    if (cmd == "cluster") {
+      const size_t n = strtoull(argv[3], nullptr, 10);
+      d = atoi(argv[4]);
+      vector<float> x = read_f32(argv[2], n * d);
+      v = rows_to_abundance(x, n, d);
+      argi = 5;
+    } else {
+      d = atoi(argv[3]);
+      IOMat::ReadClusterAll(&v, d, argv[2], false);
+      argi = 4;
+    }
+    const float min_sim = (float)atof(argv[argi]);
+    const int iters = atoi(argv[argi + 1]);
+    const int bthr = atoi(argv[argi + 2]);
+    Cluster(&v, min_sim, iters, 1, d, bthr, true);
+    save(&v, argv[argi + 3]);
+    return 0;
+  }
+  if (cmd == "convert") {
+    const size_t n = strtoull(argv[3], nullptr, 10);
+    const int d = atoi(argv[4]);
+    vector<uint16_t> counts((size_t)n * d);
+    FILE* f = fopen(argv[2], "rb");
+    if (!f || fread(counts.data(), 2, counts.size(), f) != counts.size()) { fprintf(stderr, "read\n"); return 2; }
+    fclose(f);
+    vector<float> vk = read_f32(argv[5], d);
+    vector<float_t> v_kmers(vk.begin(), vk.end());
+    vector<uint16_t*> ary(d);
+    for (int j = 0; j < d; ++j) ary[j] = counts.data() + (size_t)j * n;
+    vector<Abundance*> v;
+    IOMat::convertHTMat(ary.data(), v_kmers, d, false, n, 0, &v);
+    save(&v, argv[6]);
+    return 0;
+  }
+  fprintf(stderr, "unknown command %s\n", cmd.c_str());
+  return 1;
+}
