@@ -1,0 +1,250 @@
+"""Benchmark: the kmerLSH main LSH+cluster loop on the gfx950 engine.
+
+Metric (BASELINE.json): k-mers·iterations/s of the main Cluster() loop
+(reference app/kmerLSH.cc:490, function/cluster.cc:181-340) = N_0 * I / T_loop.
+
+Workload (BASELINE.json configs[1], "C2"): 10M k-mers x 64 samples, -I 500 -N 0.80.  Input is
+klsh-synth v1 (seed 11 + rank), converted on the GPU (mode C, convertHTMat) and
+put through the reference's init pass (one iteration at 0.95, bucket threshold 1e5) before timing;
+the timed step is the main loop: restore the post-init state (device-to-device) and run all
+500 iterations (bucket threshold 1e6).  Inputs are resident in HBM when timing starts.
+
+Multi-GPU: one process per GPU (torch.distributed.run).  The loop does not shard without an
+exchange step; this round every rank clusters its own independent matrix
+(replicas, weak scaling, no data-path collective).  Barrier + max-over-ranks timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c4|c5]
+                    [--cpu-baseline auto|reference|port|none]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "k-mers·iterations/sec (LSH+cluster loop), 10M k-mers × 64 samples"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (kmers, samples, iterations, min_similarity, description)
+    "c1": (100_000, 8, 10, 0.80, "C1: 100K k-mers x 8 samples, -I 10 -N 0.80"),
+    "c2": (10_000_000, 64, 500, 0.80, "C2: 10M k-mers x 64 samples, -I 500 -N 0.80"),
+    "c4": (100_000_000, 32, 100, 0.80, "C4: 100M k-mers x 32 samples, -I 100 -N 0.80"),
+    "c5": (10_000_000, 512, 500, 0.80, "C5: 10M k-mers x 512 samples, -I 500 -N 0.80"),
+}
+
+
+def log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # timing scalars only: the data path has no collective (replicas)
+        dist.init_process_group(backend="gloo", rank=rank, world_size=world)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(world, value: float) -> float:
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def prepare(eng, n, d, seed):
+    """synth counts -> GPU convert -> init pass; returns (rng counter, kept rows, init stats)."""
+    from kmerlsh_amd import _native
+
+    t0 = time.time()
+    counts, cov = _native.synth_counts(n, d, seed=seed)
+    # kmer_count.log carries "%f" coverages; v_kmers = float(cov) / float(kmap_size)
+    cov_f = np.array([np.float32(float("%f" % c)) for c in cov], dtype=np.float32)
+    v_kmers = (cov_f / np.float32(n)).astype(np.float32)
+    log(f"synth {n}x{d} in {time.time() - t0:.1f}s")
+    eng.load_counts(counts, v_kmers)
+    del counts
+    kept, _ = eng.count()
+    _, counter, st0 = eng.cluster(0.80, 1, 100_000, 12345, 0)  # init pass (app/kmerLSH.cc:323)
+    eng.snapshot()
+    log(f"init pass: {kept} -> {st0['n_final']} rows ({st0['wall_ms']:.1f} ms)")
+    return counter, kept, st0
+
+
+def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter):
+    """Reference (oracle/_ref) or oracle port timed on this host over a bounded sample: the first
+    3 iterations of the same main loop on the same post-init rows (same threshold schedule)."""
+    if mode == "none":
+        return None
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    threads = min(16, os.cpu_count() or 1)
+    k = 3
+    step = np.float32((np.float32(0.95) - np.float32(min_sim)) / np.float32(iters))
+    sample_min = float(np.float32(0.95) - np.float32(k) * step)
+    eng.restore()
+    rows, off, ids = eng.result()
+    desc = (f"first {k} of {iters} iterations of the main loop on the same post-init "
+            f"{rows.shape[0]}x{d} rows (threshold 0.95 falling by {float(step):.6g})")
+    kind = None
+    if mode in ("auto", "reference") and os.path.exists(harness):
+        kind = "reference"
+    elif mode in ("auto", "port"):
+        kind = "port"
+    if kind is None:
+        return None
+    if kind == "reference":
+        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
+            src = os.path.join(tmp, "rows.f32")
+            rows.astype("<f4").tofile(src)
+            off.astype("<u8").tofile(src + ".off")
+            ids.astype("<u8").tofile(src + ".ids")
+            env = dict(os.environ, OMP_THREAD_LIMIT=str(threads), OMP_NUM_THREADS=str(threads),
+                       KLSH_SEED="12345")
+            log(f"cpu baseline: reference harness, {threads} threads, {desc}")
+            out = subprocess.run([harness, "cluster_w", src, src + ".off", src + ".ids",
+                                  str(rows.shape[0]), str(d), repr(sample_min), str(k), "1000000",
+                                  os.path.join(tmp, "out")], env=env, check=True,
+                                 capture_output=True, text=True, timeout=900).stdout
+        m = re.findall(r"hash\+cluster takes \(secs\): ([0-9.eE+-]+)", out)
+        secs = float(m[-1])
+    else:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import klsh_oracle
+
+        log(f"cpu baseline: oracle port, {threads} threads, {desc}")
+        t0 = time.perf_counter()
+        klsh_oracle.cluster(rows, sample_min, k, 1_000_000, 12345, counter, off, ids, threads)
+        secs = time.perf_counter() - t0
+    return {"value": n0 * k / secs, "unit": "k-mers·iterations/s", "cores": threads,
+            "kind": kind, "sample": desc, "seconds": secs}
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        data = json.load(f)
+    return data.get(config)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "none"])
+    args = ap.parse_args()
+
+    world, rank, local = dist_setup()
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
+    n0, d, iters, min_sim, desc = CONFIGS[args.config]
+    from kmerlsh_amd import _native
+
+    eng = _native.Engine(local)
+    counter0, kept, _ = prepare(eng, n0, d, seed=11 + rank)
+
+    def step():
+        eng.restore()
+        _, _, st = eng.cluster(min_sim, iters, 1_000_000, 12345, counter0)
+        return st
+
+    for w in range(args.warmup):
+        st = step()
+        log(f"warmup {w}: {st['wall_ms']:.1f} ms, {st['iterations']} iterations, "
+            f"final {st['n_final']} clusters")
+    barrier(world)
+    t0 = time.perf_counter()
+    stats = [step() for _ in range(args.steps)]
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(world, elapsed)
+
+    if rank != 0:
+        return
+    value = world * n0 * iters * args.steps / elapsed
+    agg = {k: sum(s[k] for s in stats) for k in stats[0]}
+    phases = {p: agg[p + "_ms"] / args.steps for p in ("project", "sort", "merge", "compact", "host")}
+    # dominant kernel: the projection (k_project<64>) unless another phase dominates
+    launches = agg["project_launches"]
+    proj_bytes = agg["sum_rows"] * (4 * d + 8)      # row read + slot read + key write
+    avg_ms = agg["project_ms"] / max(1, launches)
+    achieved = (proj_bytes / max(1, launches)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = pmc_traffic(args.config)
+    roofline = {
+        "kernel": f"k_project<{d}>" if d in (8, 16, 32, 64) else "k_project_generic",
+        "bound": "hbm",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "traffic": traffic,
+        "bytes_per_launch": proj_bytes / max(1, launches),
+        "avg_launch_ms": avg_ms,
+        "launches_per_step": launches / args.steps,
+    }
+    cpu = None
+    if world == 1:
+        try:
+            cpu = cpu_baseline(eng, args.cpu_baseline, n0, d, iters, min_sim, counter0)
+        except Exception as e:  # the baseline is reported, never required
+            log(f"cpu baseline failed: {e}")
+    line = {
+        "metric": METRIC if args.config == "c2" else f"k-mers·iterations/sec, {desc}",
+        "value": value,
+        "unit": "k-mers·iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1000.0,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic klsh-synth v1 (seed 11+rank), {kept} rows kept of {n0}",
+        "config": {"workload": desc + " (main Cluster loop after the init pass)", "kmers": n0,
+                   "samples": d, "iterations": iters, "min_similarity": min_sim,
+                   "bucket_size_threshold": 1_000_000,
+                   "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "phases_ms_per_step": phases,
+        "rows_projected_per_step": agg["sum_rows"] / args.steps,
+        "final_clusters": stats[-1]["n_final"],
+        "nested_calls_per_step": agg["nested_calls"] / args.steps,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

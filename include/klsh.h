@@ -1,0 +1,131 @@
+/* klsh — MI355X-native LSH k-mer clustering engine: the C-ABI drop-in boundary.
+ *
+ * The reference (wthanone/kmerLSH) has no plugin/FFI layer; its seam for this hot path is the C++
+ * function
+ *     void Cluster(vector<Abundance*>* rows, float min_similarity, int cluster_iteration,
+ *                  unsigned threads_to_use, int dim, int bucket_size_threshold, bool verbose)
+ * (reference function/cluster.h:42, body function/cluster.cc:181-340), called from
+ * app/kmerLSH.cc:323 (init pass), :377 (re-cluster passes) and :490 (main loop).  The entry points
+ * below replace that call and the functions on its path; include/klsh_cluster.hpp wraps them back
+ * into the reference's exact signature.
+ *
+ * Conventions: every int-returning call returns 0 or a negative KLSH_E_* code; no C++ exception
+ * crosses this boundary.  The library owns device memory; the caller owns every host buffer
+ * (size queries first: klsh_count).  One context per host thread; not re-entrant on one context.
+ * All host pointers are plain host memory; nothing here takes or returns a torch type.
+ *
+ * Determinism: results equal the reference at -T 1 (OMP_THREAD_LIMIT=1) with the seeding
+ * convention of SURVEY.md §8(c): hyperplane k of a run is drawn from
+ * std::mt19937(seed_base + k*2654435761) with std::normal_distribution<double>(0,1), cast to
+ * float.  `rng_counter` carries k across calls (init pass, then main loop).
+ */
+#ifndef KLSH_H
+#define KLSH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KLSH_OK 0
+#define KLSH_E_ARG (-1)      /* bad argument (null pointer, d <= 0, sizes) */
+#define KLSH_E_HIP (-2)      /* a HIP runtime call failed (message: klsh_last_error) */
+#define KLSH_E_NOMEM (-3)    /* device or host allocation failed */
+#define KLSH_E_STATE (-4)    /* call out of order (e.g. klsh_cluster before a load) */
+#define KLSH_E_NODEVICE (-5) /* no gfx950 device visible: the engine has no CPU fallback */
+#define KLSH_E_RANGE (-6)    /* a size exceeds what the engine supports (rows >= 2^32, d > 4096) */
+
+typedef struct klsh_ctx klsh_ctx;
+
+/* Per-call statistics (all times are milliseconds). */
+typedef struct klsh_stats {
+  uint64_t iterations;     /* iterations run */
+  uint64_t sum_rows;       /* sum over iterations of N_t (rows projected) */
+  uint64_t sum_merges;     /* sum over iterations of M_t = N_t - N_{t+1} */
+  uint64_t sum_proj_bits;  /* sum over iterations of N_t * h_t (row-hyperplane dot products) */
+  uint64_t nested_calls;   /* oversize buckets sent through nestedCluster */
+  uint64_t hyperplanes;    /* hyperplanes drawn by this call */
+  uint64_t n_final;        /* live rows after the call */
+  uint64_t project_launches;
+  double wall_ms;          /* host wall clock of the whole call */
+  double project_ms;       /* HIP-event time of the projection kernel launches */
+  double sort_ms;          /* HIP-event time of the bucket (radix) sort */
+  double merge_ms;         /* HIP-event time of the greedy in-bucket merge kernels */
+  double compact_ms;       /* HIP-event time of the survivor compaction */
+  double host_ms;          /* host-side hyperplane generation */
+} klsh_stats;
+
+/* ---- lifetime ------------------------------------------------------------------------------- */
+/* Create a context on HIP device `device` (ordinal).  *err receives the status. */
+klsh_ctx* klsh_create(int device, int* err);
+void klsh_destroy(klsh_ctx* ctx);
+const char* klsh_last_error(void);  /* thread-local text for the last failure */
+const char* klsh_version(void);
+
+/* ---- loading the rows (replaces building vector<Abundance*>) ---------------------------------- */
+/* rows: n x d fp32 row-major (reference common/abundance.h:18-36, `_values`).
+ * member_offsets (n+1) / member_ids: each row's id list (`_ids`); NULL member_offsets means row i
+ * is the singleton {member_ids ? member_ids[i] : i} (reference io/ioMatrix.cc:373). */
+int klsh_load_rows(klsh_ctx* ctx, const float* rows, uint64_t n, int d,
+                   const uint64_t* member_offsets, const uint64_t* member_ids);
+
+/* Mode-C producer on the GPU (reference io/ioHT.cc:59-81 ReadHT + io/ioMatrix.cc:353-408
+ * convertHTMat): counts is the whole sample-major kmer_count.bin image (d columns of n_total
+ * uint16), the batch is rows [batch_offset, batch_offset+batch_size); v_kmers[j] =
+ * coverage_j / kmap_size as the reference computes it (app/kmerLSH.cc:471-482).  Rows with
+ * sum(count) <= 0.1*d are dropped; ids are batch_offset + i. */
+int klsh_load_counts(klsh_ctx* ctx, const uint16_t* counts, uint64_t n_total,
+                     uint64_t batch_offset, uint64_t batch_size, int d, const float* v_kmers);
+
+/* Keep a device-side copy of the loaded state / restore it (for repeated timing; both are
+ * device-to-device copies). */
+int klsh_snapshot(klsh_ctx* ctx);
+int klsh_restore(klsh_ctx* ctx);
+
+/* ---- the hot path ------------------------------------------------------------------------------ */
+/* Cluster() (reference function/cluster.cc:181-340) over the loaded rows: `iterations` rounds of
+ * hyperplane draw -> sign-hash every live row -> stable bucket -> greedy cosine merge per bucket
+ * (nestedCluster for buckets above bucket_size_threshold), threshold falling from 0.95 toward
+ * min_similarity.  nt_trace (may be NULL) receives N_t at the start of each iteration.
+ * stats may be NULL. */
+int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket_size_threshold,
+                 uint32_t seed_base, uint64_t* rng_counter, uint64_t* nt_trace, klsh_stats* stats);
+
+/* ---- results ---------------------------------------------------------------------------------- */
+int klsh_count(klsh_ctx* ctx, uint64_t* n_rows, uint64_t* n_members);
+/* Canonical order: rows (n_rows*d), member_offsets (n_rows+1), member_ids (n_members); any may
+ * be NULL. */
+int klsh_result(klsh_ctx* ctx, float* rows, uint64_t* member_offsets, uint64_t* member_ids);
+
+/* ---- path functions, exposed for parity tests ------------------------------------------------- */
+/* Hash::LSH::random_projection(row, table) (reference hash/lshash.cc:44-59) for n rows on the
+ * GPU: keys[i] = MSB-first sign bits of the h hyperplanes (table: h x d, row-major). */
+int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const float* table, int h,
+                   uint32_t* keys);
+/* p_cluster (reference function/cluster.cc:56-87) over the loaded rows taken as ONE bucket in
+ * load order, at threshold thr.  Afterwards klsh_count/klsh_result give the survivors. */
+int klsh_pcluster(klsh_ctx* ctx, float thr);
+/* LSH::generateHashTable (reference hash/lshash.cc:36-42) under the seeding convention:
+ * h hyperplanes of d floats starting at draw index *rng_counter (advanced by h). */
+int klsh_hyperplanes(uint32_t seed_base, uint64_t* rng_counter, int h, int d, float* table);
+/* The merge test's sqrt and division exactly as the kernels evaluate them (sqrt_out[i] =
+ * sqrtf(a[i]), div_out[i] = a[i] / b[i]); for checking IEEE correct rounding on the device. */
+int klsh_fp_selftest(klsh_ctx* ctx, const float* a, const float* b, uint64_t n, float* sqrt_out,
+                     float* div_out);
+
+/* ---- synthetic workload (klsh-synth v1) ------------------------------------ */
+/* Host-side, deterministic on any machine (integer hashing + glibc exp/log/sqrt): fills counts
+ * (sample-major d x n uint16, the kmer_count.bin layout) and coverage[d] = sum over i of ln(c)
+ * for c > 0, summed in double in ascending i (the kmer_count.log convention).  Rows belong to
+ * `genomes` groups (n/50 if 0): profile(g,s) = exp(2 + z), z ~ N(0,1); multiplicity m in {1,2};
+ * count = min(Poisson(profile*m), 65535) (inversion below 30, normal approximation above).
+ * threads <= 0: all host threads. */
+int klsh_synth_counts(uint64_t n, int d, uint64_t seed, uint64_t genomes, int threads,
+                      uint16_t* counts, double* coverage);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

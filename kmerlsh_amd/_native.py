@@ -1,0 +1,246 @@
+"""ctypes binding of the C-ABI engine library (include/klsh.h -> kmerlsh_amd/lib/libklsh.so).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C kmerlsh_amd/csrc``).
+There is no fallback: if the library is missing, or no gfx950 device is visible, every entry point
+raises.  Loading the library itself needs no GPU (the symbol checks in tests/ run on CPU).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libklsh.so")
+CLI_PATH = os.path.join(_HERE, "bin", "kmerLSH")
+
+KLSH_OK = 0
+ERRORS = {
+    -1: "KLSH_E_ARG",
+    -2: "KLSH_E_HIP",
+    -3: "KLSH_E_NOMEM",
+    -4: "KLSH_E_STATE",
+    -5: "KLSH_E_NODEVICE",
+    -6: "KLSH_E_RANGE",
+}
+
+# Every symbol include/klsh.h declares (tests/test_native_lib.py checks the .so exports them).
+EXPORTED = (
+    "klsh_create", "klsh_destroy", "klsh_last_error", "klsh_version", "klsh_load_rows",
+    "klsh_load_counts", "klsh_snapshot", "klsh_restore", "klsh_cluster", "klsh_count",
+    "klsh_result", "klsh_hash_keys", "klsh_pcluster", "klsh_hyperplanes", "klsh_fp_selftest",
+    "klsh_synth_counts",
+)
+
+
+class KlshStats(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_uint64),
+        ("sum_rows", ctypes.c_uint64),
+        ("sum_merges", ctypes.c_uint64),
+        ("sum_proj_bits", ctypes.c_uint64),
+        ("nested_calls", ctypes.c_uint64),
+        ("hyperplanes", ctypes.c_uint64),
+        ("n_final", ctypes.c_uint64),
+        ("project_launches", ctypes.c_uint64),
+        ("wall_ms", ctypes.c_double),
+        ("project_ms", ctypes.c_double),
+        ("sort_ms", ctypes.c_double),
+        ("merge_ms", ctypes.c_double),
+        ("compact_ms", ctypes.c_double),
+        ("host_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class KlshError(RuntimeError):
+    pass
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libklsh.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KlshError(
+            f"{LIB_PATH} is missing: the gfx950 engine has no CPU fallback; "
+            "build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "klsh_create": (_P, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+        "klsh_destroy": (None, [_P]),
+        "klsh_last_error": (ctypes.c_char_p, []),
+        "klsh_version": (ctypes.c_char_p, []),
+        "klsh_load_rows": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, _P, _P]),
+        "klsh_load_counts": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64,
+                                            ctypes.c_uint64, ctypes.c_int, _P]),
+        "klsh_snapshot": (ctypes.c_int, [_P]),
+        "klsh_restore": (ctypes.c_int, [_P]),
+        "klsh_cluster": (ctypes.c_int, [_P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_uint32, _u64p, _P, _P]),
+        "klsh_count": (ctypes.c_int, [_P, _u64p, _u64p]),
+        "klsh_result": (ctypes.c_int, [_P, _P, _P, _P]),
+        "klsh_hash_keys": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, _P,
+                                          ctypes.c_int, _P]),
+        "klsh_pcluster": (ctypes.c_int, [_P, ctypes.c_float]),
+        "klsh_hyperplanes": (ctypes.c_int, [ctypes.c_uint32, _u64p, ctypes.c_int,
+                                            ctypes.c_int, _P]),
+        "klsh_fp_selftest": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P]),
+        "klsh_synth_counts": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_int, _P, _P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != KLSH_OK:
+        msg = load_library().klsh_last_error().decode(errors="replace")
+        raise KlshError(f"{what} failed: {ERRORS.get(rc, rc)}: {msg}")
+
+
+def hyperplanes(seed: int, counter: int, h: int, d: int) -> tuple[np.ndarray, int]:
+    """LSH::generateHashTable under the seeding convention (host; no GPU needed)."""
+    lib = load_library()
+    out = np.zeros((max(h, 0), d), dtype=np.float32)
+    c = ctypes.c_uint64(counter)
+    _check(lib.klsh_hyperplanes(seed, ctypes.byref(c), h, d, _ptr(out)), "klsh_hyperplanes")
+    return out, c.value
+
+
+def synth_counts(n: int, d: int, seed: int, genomes: int = 0, threads: int = 0):
+    """klsh-synth v1 (host): sample-major (d, n) uint16 counts and per-sample coverage."""
+    lib = load_library()
+    counts = np.empty((d, n), dtype=np.uint16)
+    cov = np.empty(d, dtype=np.float64)
+    _check(lib.klsh_synth_counts(n, d, seed, genomes, threads, _ptr(counts), _ptr(cov)),
+           "klsh_synth_counts")
+    return counts, cov
+
+
+class Engine:
+    """One device context (``klsh_ctx``)."""
+
+    def __init__(self, device: int = 0):
+        lib = load_library()
+        err = ctypes.c_int(0)
+        self._ctx = lib.klsh_create(device, ctypes.byref(err))
+        if not self._ctx:
+            _check(err.value or -2, "klsh_create")
+        self._lib = lib
+        self.d = 0
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.klsh_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- loading
+    def load_rows(self, rows: np.ndarray, member_offsets: np.ndarray | None = None,
+                  member_ids: np.ndarray | None = None) -> None:
+        rows = np.ascontiguousarray(rows, dtype=np.float32)
+        n, d = rows.shape
+        mo = None if member_offsets is None else np.ascontiguousarray(member_offsets, np.uint64)
+        mi = None if member_ids is None else np.ascontiguousarray(member_ids, np.uint64)
+        _check(self._lib.klsh_load_rows(self._ctx, _ptr(rows), n, d, _ptr(mo), _ptr(mi)),
+               "klsh_load_rows")
+        self.d = d
+
+    def load_counts(self, counts: np.ndarray, v_kmers: np.ndarray, batch_offset: int = 0,
+                    batch_size: int | None = None) -> None:
+        counts = np.ascontiguousarray(counts, dtype=np.uint16)
+        d, n_total = counts.shape
+        if batch_size is None:
+            batch_size = n_total - batch_offset
+        vk = np.ascontiguousarray(v_kmers, dtype=np.float32)
+        _check(self._lib.klsh_load_counts(self._ctx, _ptr(counts), n_total, batch_offset,
+                                          batch_size, d, _ptr(vk)), "klsh_load_counts")
+        self.d = d
+
+    def snapshot(self) -> None:
+        _check(self._lib.klsh_snapshot(self._ctx), "klsh_snapshot")
+
+    def restore(self) -> None:
+        _check(self._lib.klsh_restore(self._ctx), "klsh_restore")
+
+    # ---- hot path
+    def cluster(self, min_similarity: float, iterations: int, bucket_size_threshold: int,
+                seed: int = 12345, counter: int = 0):
+        """Returns (trace of N_t, new rng counter, stats dict)."""
+        c = ctypes.c_uint64(counter)
+        trace = np.zeros(max(iterations, 1), dtype=np.uint64)
+        st = KlshStats()
+        _check(self._lib.klsh_cluster(self._ctx, ctypes.c_float(min_similarity), iterations,
+                                      bucket_size_threshold, seed, ctypes.byref(c), _ptr(trace),
+                                      ctypes.byref(st)), "klsh_cluster")
+        return trace[: st.iterations], c.value, st.as_dict()
+
+    def pcluster(self, thr: float) -> None:
+        _check(self._lib.klsh_pcluster(self._ctx, ctypes.c_float(thr)), "klsh_pcluster")
+
+    def hash_keys(self, rows: np.ndarray, table: np.ndarray) -> np.ndarray:
+        rows = np.ascontiguousarray(rows, dtype=np.float32)
+        table = np.ascontiguousarray(table, dtype=np.float32)
+        n, d = rows.shape
+        h = table.shape[0]
+        keys = np.zeros(n, dtype=np.uint32)
+        _check(self._lib.klsh_hash_keys(self._ctx, _ptr(rows), n, d, _ptr(table), h,
+                                        _ptr(keys)), "klsh_hash_keys")
+        return keys
+
+    def fp_selftest(self, a: np.ndarray, b: np.ndarray):
+        a = np.ascontiguousarray(a, np.float32)
+        b = np.ascontiguousarray(b, np.float32)
+        s = np.zeros_like(a)
+        q = np.zeros_like(a)
+        _check(self._lib.klsh_fp_selftest(self._ctx, _ptr(a), _ptr(b), a.size, _ptr(s), _ptr(q)),
+               "klsh_fp_selftest")
+        return s, q
+
+    # ---- results
+    def count(self) -> tuple[int, int]:
+        n = ctypes.c_uint64(0)
+        m = ctypes.c_uint64(0)
+        _check(self._lib.klsh_count(self._ctx, ctypes.byref(n), ctypes.byref(m)), "klsh_count")
+        return n.value, m.value
+
+    def result(self):
+        """(rows (n, d) float32, member_offsets (n+1,) uint64, member_ids (m,) uint64)."""
+        n, m = self.count()
+        rows = np.zeros((n, self.d), dtype=np.float32)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        ids = np.zeros(m, dtype=np.uint64)
+        _check(self._lib.klsh_result(self._ctx, _ptr(rows), _ptr(off), _ptr(ids)),
+               "klsh_result")
+        return rows, off, ids

@@ -1,0 +1,719 @@
+// Host engine behind the C ABI (include/klsh.h): device state, the per-iteration launch
+// sequence of Cluster() (reference function/cluster.cc:181-340), nestedCluster orchestration
+// (:89-178) and result extraction.  The arithmetic of the path runs only in the gfx950 kernels
+// (klsh_kernels.hip); there is no CPU fallback — without a gfx950 device klsh_create fails.
+//
+// Per LSH iteration t (N_t live rows, h_t = floor(log2 N_t)):
+//   1. hyperplanes k_t .. k_t+h_t-1 (pre-drawn on the host, uploaded once per call)
+//   2. k_project: key of every live row, in canonical order
+//   3. radix sort (key, slot): the stable bucket order of merge_hashtable
+//   4. k_merge_small / k_merge_large: greedy p_cluster in every bucket, in place
+//   5. compaction of survivors -> canonical order of iteration t+1
+//   6. one device->host copy of the counters (N_{t+1}, oversize buckets) and a stream sync
+// Oversize buckets (> bucket_size_threshold) are then re-hashed with fresh hyperplanes drawn in
+// ascending bucket order (the reference's T=1 RNG order), sorted, merged, and 5 is redone.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "klsh.h"
+#include "klsh_internal.h"
+
+extern "C" {
+uint32_t klsh_host_seed(uint32_t base, uint64_t k);
+void klsh_host_hyperplanes(uint32_t base, uint64_t k0, uint64_t count, int d, int stride,
+                           float* out, int threads);
+}
+
+using klsh::Counters;
+using klsh::Rows;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define KLSH_HIP(call)                                                                   \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(KLSH_E_HIP, std::string(#call) + " -> " + hipGetErrorString(e_));      \
+  } while (0)
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+int floor_log2(uint64_t n) { return (int)std::floor(std::log2((double)n)); }  // cluster.cc:194
+
+template <class T>
+int dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  if (hipMalloc((void**)p, sizeof(T) * count) != hipSuccess) {
+    *p = nullptr;
+    return fail(KLSH_E_NOMEM, "hipMalloc of " + std::to_string(sizeof(T) * count) + " bytes");
+  }
+  return 0;
+}
+
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+struct Snapshot {
+  bool valid = false;
+  uint64_t n_live = 0;
+  float* x = nullptr;
+  float* nrm = nullptr;
+  uint32_t *cnt = nullptr, *head = nullptr, *tail = nullptr, *nxt = nullptr, *order = nullptr;
+};
+
+}  // namespace
+
+struct klsh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[8] = {};
+
+  // sizes
+  int d = 0, dp = 0;
+  uint64_t slots = 0, members = 0, n_live = 0;
+  uint64_t cap_slots = 0, cap_members = 0;
+  int cap_dp = 0;
+  bool loaded = false;
+
+  // device state
+  Rows rows{};
+  uint32_t* order = nullptr;  // canonical live slots
+  uint32_t* alt = nullptr;    // second slot buffer (sort / compaction ping-pong)
+  uint32_t* keys = nullptr;
+  uint32_t* keys2 = nullptr;
+  uint32_t* nk1 = nullptr;    // nested scratch
+  uint32_t* nk2 = nullptr;
+  uint32_t* nv2 = nullptr;
+  uint32_t* hist = nullptr;
+  uint32_t* tile_sums = nullptr;
+  uint32_t* large_list = nullptr;
+  uint2* over_list = nullptr;
+  Counters* ctr = nullptr;
+  Counters* h_ctr = nullptr;  // pinned
+  float* W = nullptr;         // hyperplane pool on the device, [k - w_k0][dp]
+  uint64_t w_k0 = 0, w_count = 0, w_cap = 0, w_alloc = 0;
+  uint32_t w_base = 0;
+  int w_dp = 0, w_d = 0;
+
+  // host
+  std::vector<uint64_t> ids;  // member node -> k-mer id
+  Snapshot snap;
+
+  ~klsh_ctx() { release(); }
+
+  void release_state() {
+    dfree(rows.x); dfree(rows.nrm); dfree(rows.cnt); dfree(rows.head); dfree(rows.tail);
+    dfree(rows.nxt); dfree(order); dfree(alt); dfree(keys); dfree(keys2); dfree(nk1);
+    dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(large_list); dfree(over_list);
+    cap_slots = cap_members = 0;
+    cap_dp = 0;
+    drop_snapshot();
+  }
+  void drop_snapshot() {
+    dfree(snap.x); dfree(snap.nrm); dfree(snap.cnt); dfree(snap.head); dfree(snap.tail);
+    dfree(snap.nxt); dfree(snap.order);
+    snap.valid = false;
+  }
+  void release() {
+    release_state();
+    dfree(W);
+    dfree(ctr);
+    if (h_ctr) (void)hipHostFree(h_ctr);
+    h_ctr = nullptr;
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    if (stream) (void)hipStreamDestroy(stream);
+    stream = nullptr;
+  }
+
+  // (Re)allocate device state for `ns` slots, `nm` member nodes, row width d.
+  int reserve(uint64_t ns, uint64_t nm, int d_) {
+    if (ns >= 0xFFFFFFF0ull || nm >= 0xFFFFFFF0ull) return fail(KLSH_E_RANGE, "rows >= 2^32");
+    if (d_ <= 0 || d_ > 4096) return fail(KLSH_E_RANGE, "d must be in [1, 4096]");
+    const int dp_ = (d_ + 3) & ~3;
+    if (ns <= cap_slots && nm <= cap_members && dp_ <= cap_dp) {
+      d = d_;
+      dp = dp_;
+      rows.d = d;
+      rows.dp = dp;
+      drop_snapshot();
+      return 0;
+    }
+    release_state();
+    const uint64_t s = std::max<uint64_t>(ns, 1), m = std::max<uint64_t>(nm, 1);
+    int e = 0;
+    if ((e = dalloc(&rows.x, s * dp_)) || (e = dalloc(&rows.nrm, s)) || (e = dalloc(&rows.cnt, s)) ||
+        (e = dalloc(&rows.head, s)) || (e = dalloc(&rows.tail, s)) || (e = dalloc(&rows.nxt, m)) ||
+        (e = dalloc(&order, s)) || (e = dalloc(&alt, s)) || (e = dalloc(&keys, s)) ||
+        (e = dalloc(&keys2, s)) || (e = dalloc(&nk1, s)) || (e = dalloc(&nk2, s)) ||
+        (e = dalloc(&nv2, s)) ||
+        (e = dalloc(&hist, 256 * ((s + klsh::kRadixTile - 1) / klsh::kRadixTile) + 256)) ||
+        (e = dalloc(&tile_sums, (256 * s) / klsh::kScanTile + 1024)) ||
+        (e = dalloc(&large_list, s / (klsh::kSmallBucket + 1) + 64)) ||
+        (e = dalloc(&over_list, s + 64))) {
+      release_state();
+      return e;
+    }
+    cap_slots = s;
+    cap_members = m;
+    cap_dp = dp_;
+    d = d_;
+    dp = dp_;
+    rows.d = d;
+    rows.dp = dp;
+    return 0;
+  }
+
+  // Make hyperplanes [k0, k0+count) of stream `base` resident on the device (drawn on the host).
+  // The resident window [w_k0, w_k0 + w_count) only grows forward; anything else restarts it.
+  int ensure_hyperplanes(uint32_t base, uint64_t k0, uint64_t count, double* host_ms) {
+    if (count == 0) return 0;
+    const bool same_stream = W && w_base == base && w_dp == dp && w_d == d;
+    if (same_stream && k0 >= w_k0 && k0 + count <= w_k0 + w_count) return 0;
+    const double t0 = now_ms();
+    if (!(same_stream && k0 >= w_k0 && k0 + count <= w_k0 + w_cap)) {
+      const uint64_t cap = std::max<uint64_t>({count, 4096, w_cap});
+      if (!W || cap * (uint64_t)dp > w_alloc) {
+        dfree(W);
+        if (int e = dalloc(&W, cap * (uint64_t)dp)) return e;
+        w_alloc = cap * (uint64_t)dp;
+      }
+      w_cap = w_alloc / (uint64_t)dp;
+      w_k0 = k0;
+      w_count = 0;
+      w_base = base;
+      w_dp = dp;
+      w_d = d;
+    }
+    const uint64_t start = w_k0 + w_count, n = k0 + count - start;
+    std::vector<float> host((size_t)n * dp, 0.0f);
+    klsh_host_hyperplanes(base, start, n, d, dp, host.data(), 0);
+    KLSH_HIP(hipMemcpyAsync(W + (start - w_k0) * dp, host.data(), sizeof(float) * host.size(),
+                            hipMemcpyHostToDevice, stream));
+    KLSH_HIP(hipStreamSynchronize(stream));
+    w_count += n;
+    if (host_ms) *host_ms += now_ms() - t0;
+    return 0;
+  }
+  const float* hyperplane_ptr(uint64_t k) const { return W + (k - w_k0) * (uint64_t)dp; }
+
+  int sync_counters() {
+    KLSH_HIP(hipMemcpyAsync(h_ctr, ctr, sizeof(Counters), hipMemcpyDeviceToHost, stream));
+    KLSH_HIP(hipStreamSynchronize(stream));
+    return 0;
+  }
+};
+
+namespace {
+
+float elapsed(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0f;
+  return ms;
+}
+
+}  // namespace
+
+// ===================================================================================== C ABI ===
+extern "C" {
+
+const char* klsh_last_error(void) { return g_err.c_str(); }
+const char* klsh_version(void) { return "klsh-mi355x 0.1 (gfx950)"; }
+
+klsh_ctx* klsh_create(int device, int* err) {
+  auto set = [&](int e) {
+    if (err) *err = e;
+  };
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    fail(KLSH_E_NODEVICE, "no HIP device visible (the engine has no CPU fallback)");
+    set(KLSH_E_NODEVICE);
+    return nullptr;
+  }
+  if (device < 0 || device >= count) {
+    fail(KLSH_E_ARG, "device ordinal out of range");
+    set(KLSH_E_ARG);
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
+      std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+    fail(KLSH_E_NODEVICE, std::string("device is not gfx950: ") + prop.gcnArchName);
+    set(KLSH_E_NODEVICE);
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    fail(KLSH_E_HIP, "hipSetDevice");
+    set(KLSH_E_HIP);
+    return nullptr;
+  }
+  klsh_ctx* c = new klsh_ctx();
+  c->device = device;
+  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+  for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  ok = ok && hipMalloc((void**)&c->ctr, sizeof(Counters)) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) == hipSuccess;
+  if (!ok) {
+    delete c;
+    fail(KLSH_E_HIP, "stream/event/counter allocation failed");
+    set(KLSH_E_HIP);
+    return nullptr;
+  }
+  memset(c->h_ctr, 0, sizeof(Counters));
+  set(KLSH_OK);
+  return c;
+}
+
+void klsh_destroy(klsh_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  delete ctx;
+}
+
+int klsh_load_rows(klsh_ctx* ctx, const float* rows, uint64_t n, int d,
+                   const uint64_t* member_offsets, const uint64_t* member_ids) {
+  if (!ctx || (!rows && n)) return fail(KLSH_E_ARG, "null argument");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  const uint64_t m = member_offsets ? member_offsets[n] : n;
+  if (int e = ctx->reserve(n, m, d)) return e;
+  hipStream_t s = ctx->stream;
+  if (n) {
+    KLSH_HIP(hipMemsetAsync(ctx->rows.x, 0, sizeof(float) * n * ctx->dp, s));
+    KLSH_HIP(hipMemcpy2DAsync(ctx->rows.x, sizeof(float) * ctx->dp, rows, sizeof(float) * d,
+                              sizeof(float) * d, n, hipMemcpyHostToDevice, s));
+  }
+  std::vector<uint32_t> cnt(n), head(n), tail(n), nxt(m), ord(n);
+  ctx->ids.assign(m, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    ord[i] = (uint32_t)i;
+    if (member_offsets) {
+      const uint64_t a = member_offsets[i], b = member_offsets[i + 1];
+      cnt[i] = (uint32_t)(b - a);
+      head[i] = b > a ? (uint32_t)a : klsh::kNil;
+      tail[i] = b > a ? (uint32_t)(b - 1) : klsh::kNil;
+      for (uint64_t k = a; k < b; ++k) {
+        nxt[k] = k + 1 < b ? (uint32_t)(k + 1) : klsh::kNil;
+        ctx->ids[k] = member_ids ? member_ids[k] : k;
+      }
+    } else {
+      cnt[i] = 1;
+      head[i] = tail[i] = (uint32_t)i;
+      nxt[i] = klsh::kNil;
+      ctx->ids[i] = member_ids ? member_ids[i] : i;
+    }
+  }
+  if (n) {
+    KLSH_HIP(hipMemcpyAsync(ctx->rows.cnt, cnt.data(), 4 * n, hipMemcpyHostToDevice, s));
+    KLSH_HIP(hipMemcpyAsync(ctx->rows.head, head.data(), 4 * n, hipMemcpyHostToDevice, s));
+    KLSH_HIP(hipMemcpyAsync(ctx->rows.tail, tail.data(), 4 * n, hipMemcpyHostToDevice, s));
+    KLSH_HIP(hipMemcpyAsync(ctx->order, ord.data(), 4 * n, hipMemcpyHostToDevice, s));
+  }
+  if (m) KLSH_HIP(hipMemcpyAsync(ctx->rows.nxt, nxt.data(), 4 * m, hipMemcpyHostToDevice, s));
+  klsh::launch_norms(ctx->rows, (uint32_t)n, s);
+  KLSH_HIP(hipGetLastError());
+  KLSH_HIP(hipStreamSynchronize(s));
+  ctx->slots = n;
+  ctx->members = m;
+  ctx->n_live = n;
+  ctx->loaded = true;
+  return 0;
+}
+
+int klsh_load_counts(klsh_ctx* ctx, const uint16_t* counts, uint64_t n_total,
+                     uint64_t batch_offset, uint64_t batch_size, int d, const float* v_kmers) {
+  if (!ctx || !counts || !v_kmers) return fail(KLSH_E_ARG, "null argument");
+  if (batch_offset + batch_size > n_total) return fail(KLSH_E_ARG, "batch outside the matrix");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  const uint64_t bs = batch_size;
+  if (int e = ctx->reserve(bs, bs, d)) return e;
+  hipStream_t s = ctx->stream;
+  // float(log(c + 1.0)) for every uint16 count: glibc double log on the host, exact.
+  static std::vector<float> lut;
+  if (lut.empty()) {
+    lut.resize(65536);
+    for (int c = 0; c < 65536; ++c) lut[c] = (float)std::log((double)c + 1.0);
+  }
+  uint16_t* dcounts = nullptr;
+  float *dlut = nullptr, *dv = nullptr;
+  if (int e = dalloc(&dcounts, (size_t)bs * d)) return e;
+  if (int e = dalloc(&dlut, 65536)) { dfree(dcounts); return e; }
+  if (int e = dalloc(&dv, d)) { dfree(dcounts); dfree(dlut); return e; }
+  int rc = 0;
+  do {
+    if (bs) {
+      if (hipMemcpy2DAsync(dcounts, sizeof(uint16_t) * bs, counts + batch_offset,
+                           sizeof(uint16_t) * n_total, sizeof(uint16_t) * bs, d,
+                           hipMemcpyHostToDevice, s) != hipSuccess) {
+        rc = fail(KLSH_E_HIP, "count upload");
+        break;
+      }
+    }
+    if (hipMemcpyAsync(dlut, lut.data(), sizeof(float) * 65536, hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        hipMemcpyAsync(dv, v_kmers, sizeof(float) * d, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = fail(KLSH_E_HIP, "lut upload");
+      break;
+    }
+    klsh::launch_convert(ctx->rows, dcounts, (uint32_t)bs, dlut, dv, ctx->keys, ctx->order,
+                         ctx->tile_sums, ctx->ctr, s);
+    if (hipGetLastError() != hipSuccess) {
+      rc = fail(KLSH_E_HIP, "convert launch");
+      break;
+    }
+    if ((rc = ctx->sync_counters())) break;
+  } while (false);
+  (void)hipStreamSynchronize(s);
+  dfree(dcounts);
+  dfree(dlut);
+  dfree(dv);
+  if (rc) return rc;
+  ctx->ids.resize(bs);
+  for (uint64_t i = 0; i < bs; ++i) ctx->ids[i] = batch_offset + i;
+  ctx->slots = bs;
+  ctx->members = bs;
+  ctx->n_live = bs ? ctx->h_ctr->total : 0;
+  ctx->loaded = true;
+  return 0;
+}
+
+int klsh_snapshot(klsh_ctx* ctx) {
+  if (!ctx || !ctx->loaded) return fail(KLSH_E_STATE, "nothing loaded");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  Snapshot& sn = ctx->snap;
+  if (!sn.valid) {
+    int e = 0;
+    const uint64_t s = std::max<uint64_t>(ctx->slots, 1), m = std::max<uint64_t>(ctx->members, 1);
+    if ((e = dalloc(&sn.x, s * ctx->dp)) || (e = dalloc(&sn.nrm, s)) || (e = dalloc(&sn.cnt, s)) ||
+        (e = dalloc(&sn.head, s)) || (e = dalloc(&sn.tail, s)) || (e = dalloc(&sn.nxt, m)) ||
+        (e = dalloc(&sn.order, s))) {
+      ctx->drop_snapshot();
+      return e;
+    }
+  }
+  hipStream_t st = ctx->stream;
+  const uint64_t s = ctx->slots, m = ctx->members;
+  KLSH_HIP(hipMemcpyAsync(sn.x, ctx->rows.x, 4 * s * ctx->dp, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(sn.nrm, ctx->rows.nrm, 4 * s, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(sn.cnt, ctx->rows.cnt, 4 * s, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(sn.head, ctx->rows.head, 4 * s, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(sn.tail, ctx->rows.tail, 4 * s, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(sn.nxt, ctx->rows.nxt, 4 * m, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(sn.order, ctx->order, 4 * ctx->n_live, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipStreamSynchronize(st));
+  sn.n_live = ctx->n_live;
+  sn.valid = true;
+  return 0;
+}
+
+int klsh_restore(klsh_ctx* ctx) {
+  if (!ctx || !ctx->snap.valid) return fail(KLSH_E_STATE, "no snapshot");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  Snapshot& sn = ctx->snap;
+  hipStream_t st = ctx->stream;
+  const uint64_t s = ctx->slots, m = ctx->members;
+  KLSH_HIP(hipMemcpyAsync(ctx->rows.x, sn.x, 4 * s * ctx->dp, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(ctx->rows.nrm, sn.nrm, 4 * s, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(ctx->rows.cnt, sn.cnt, 4 * s, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(ctx->rows.head, sn.head, 4 * s, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(ctx->rows.tail, sn.tail, 4 * s, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(ctx->rows.nxt, sn.nxt, 4 * m, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipMemcpyAsync(ctx->order, sn.order, 4 * sn.n_live, hipMemcpyDeviceToDevice, st));
+  KLSH_HIP(hipStreamSynchronize(st));
+  ctx->n_live = sn.n_live;
+  return 0;
+}
+
+// Merge + compaction of one iteration's sorted runs, plus the nested path for oversize buckets.
+// fk/fv: sorted keys/slots (fv is one of ctx->order / ctx->alt).  Returns with the new canonical
+// order in ctx->order and ctx->n_live updated.
+static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
+                             int bucket_thr, uint32_t seed_base, uint64_t* rng_counter,
+                             klsh_stats* st, bool timed) {
+  hipStream_t s = ctx->stream;
+  uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
+  if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
+  klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->large_list, ctx->over_list,
+                     ctx->ctr, s);
+  KLSH_HIP(hipGetLastError());
+  if (timed) KLSH_HIP(hipEventRecord(ctx->ev[3], s));
+  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
+  KLSH_HIP(hipGetLastError());
+  if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
+  if (int e = ctx->sync_counters()) return e;
+  if (timed && st) {
+    st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
+    st->compact_ms += elapsed(ctx->ev[3], ctx->ev[4]);
+  }
+  const uint32_t n_over = ctx->h_ctr->n_over;
+  if (n_over > 0) {
+    // nestedCluster (cluster.cc:286-288 -> :89-178) for each oversize bucket, ascending.
+    std::vector<uint2> over(n_over);
+    KLSH_HIP(hipMemcpy(over.data(), ctx->over_list, sizeof(uint2) * n_over, hipMemcpyDeviceToHost));
+    std::sort(over.begin(), over.end(), [](const uint2& a, const uint2& b) { return a.x < b.x; });
+    for (uint32_t oi = 0; oi < n_over; ++oi) {
+      const uint32_t p = over[oi].x, b = over[oi].y;
+      const int h2 = floor_log2(b);
+      const uint64_t k = *rng_counter;
+      *rng_counter += (uint64_t)h2;
+      if (st) {
+        st->hyperplanes += (uint64_t)h2;
+        st->nested_calls += 1;
+      }
+      if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h2, st ? &st->host_ms : nullptr))
+        return e;
+      // Sub-keys carry bit 31 (main keys are < 2^h <= 2^31, so never have it) and a bit 30 that
+      // alternates between consecutive oversize regions, so no run crosses a region boundary.
+      const uint32_t key_or = 0x80000000u | ((oi & 1u) << 30);
+      klsh::launch_project(ctx->rows, fv + p, ctx->nk1, b, ctx->hyperplane_ptr(k), h2, key_or, s);
+      uint32_t *rk = nullptr, *rv = nullptr;
+      klsh::radix_sort(ctx->nk1, fv + p, ctx->nk2, ctx->nv2, b, h2, ctx->hist, ctx->tile_sums,
+                       ctx->ctr, &rk, &rv, s);
+      KLSH_HIP(hipMemcpyAsync(fk + p, rk, 4ull * b, hipMemcpyDeviceToDevice, s));
+      if (rv != fv + p) KLSH_HIP(hipMemcpyAsync(fv + p, rv, 4ull * b, hipMemcpyDeviceToDevice, s));
+      KLSH_HIP(hipMemsetAsync(&ctx->ctr->n_large, 0, sizeof(uint32_t), s));
+      klsh::launch_merge(ctx->rows, fk, fv, p, p + b, thr, -1, ctx->large_list, ctx->over_list,
+                         ctx->ctr, s);
+      KLSH_HIP(hipGetLastError());
+    }
+    klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
+    KLSH_HIP(hipGetLastError());
+    if (int e = ctx->sync_counters()) return e;
+  }
+  if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
+  ctx->n_live = ctx->h_ctr->total;
+  return 0;
+}
+
+int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket_size_threshold,
+                 uint32_t seed_base, uint64_t* rng_counter, uint64_t* nt_trace, klsh_stats* stats) {
+  if (!ctx || !rng_counter) return fail(KLSH_E_ARG, "null argument");
+  if (!ctx->loaded) return fail(KLSH_E_STATE, "klsh_cluster before a load");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  klsh_stats local{};
+  klsh_stats* st = stats ? stats : &local;
+  memset(st, 0, sizeof(*st));
+  const double t_start = now_ms();
+  hipStream_t s = ctx->stream;
+
+  // cluster.cc:190-192 (all float)
+  const float max_similarity = 0.95f;
+  const float sim_step = (max_similarity - min_similarity) / (float)iterations;
+  float threshold = max_similarity;
+
+  // Pre-draw the hyperplanes this call can need without nested buckets (h_t is non-increasing).
+  if (ctx->n_live > 0 && iterations > 0) {
+    const uint64_t hmax = (uint64_t)floor_log2(ctx->n_live);
+    if (int e = ctx->ensure_hyperplanes(seed_base, *rng_counter, hmax * (uint64_t)iterations,
+                                        &st->host_ms))
+      return e;
+  }
+
+  int it = 0;
+  for (; it < iterations; ++it) {
+    const uint64_t n = ctx->n_live;
+    if (nt_trace) nt_trace[it] = n;
+    if (n == 0) {  // the reference aborts here (cluster.cc:194 on an empty vector); no-op
+      threshold -= sim_step;
+      continue;
+    }
+    const int h = floor_log2(n);
+    const uint64_t k = *rng_counter;
+    *rng_counter += (uint64_t)h;
+    st->hyperplanes += (uint64_t)h;
+    if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h, &st->host_ms)) return e;
+
+    KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    KLSH_HIP(hipEventRecord(ctx->ev[0], s));
+    klsh::launch_project(ctx->rows, ctx->order, ctx->keys, (uint32_t)n, ctx->hyperplane_ptr(k), h,
+                         0u, s);
+    KLSH_HIP(hipGetLastError());
+    KLSH_HIP(hipEventRecord(ctx->ev[1], s));
+    uint32_t *fk = nullptr, *fv = nullptr;
+    klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n, h, ctx->hist,
+                     ctx->tile_sums, ctx->ctr, &fk, &fv, s);
+    KLSH_HIP(hipGetLastError());
+    KLSH_HIP(hipEventRecord(ctx->ev[5], s));
+    if (int e = merge_and_compact(ctx, fk, fv, (uint32_t)n, threshold, bucket_size_threshold,
+                                  seed_base, rng_counter, st, true))
+      return e;
+    st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
+    st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
+    st->project_launches += 1;
+    st->iterations += 1;
+    st->sum_rows += n;
+    st->sum_proj_bits += n * (uint64_t)h;
+    st->sum_merges += n - ctx->n_live;
+    threshold -= sim_step;
+  }
+  st->n_final = ctx->n_live;
+  st->wall_ms = now_ms() - t_start;
+  return 0;
+}
+
+int klsh_count(klsh_ctx* ctx, uint64_t* n_rows, uint64_t* n_members) {
+  if (!ctx) return fail(KLSH_E_ARG, "null ctx");
+  if (!ctx->loaded) return fail(KLSH_E_STATE, "nothing loaded");
+  if (n_rows) *n_rows = ctx->n_live;
+  if (n_members) {
+    KLSH_HIP(hipSetDevice(ctx->device));
+    // members of live rows = sum of cnt over the live slots
+    std::vector<uint32_t> ord(ctx->n_live), cnt(ctx->slots);
+    if (ctx->n_live)
+      KLSH_HIP(hipMemcpy(ord.data(), ctx->order, 4 * ctx->n_live, hipMemcpyDeviceToHost));
+    if (ctx->slots)
+      KLSH_HIP(hipMemcpy(cnt.data(), ctx->rows.cnt, 4 * ctx->slots, hipMemcpyDeviceToHost));
+    uint64_t m = 0;
+    for (uint32_t sl : ord) m += cnt[sl];
+    *n_members = m;
+  }
+  return 0;
+}
+
+int klsh_result(klsh_ctx* ctx, float* rows, uint64_t* member_offsets, uint64_t* member_ids) {
+  if (!ctx) return fail(KLSH_E_ARG, "null ctx");
+  if (!ctx->loaded) return fail(KLSH_E_STATE, "nothing loaded");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  const uint64_t n = ctx->n_live;
+  hipStream_t s = ctx->stream;
+  if (rows && n) {
+    float* tmp = nullptr;
+    if (int e = dalloc(&tmp, n * (uint64_t)ctx->d)) return e;
+    klsh::launch_gather_rows(ctx->rows, ctx->order, (uint32_t)n, tmp, s);
+    hipError_t e1 = hipMemcpyAsync(rows, tmp, sizeof(float) * n * ctx->d, hipMemcpyDeviceToHost, s);
+    hipError_t e2 = hipStreamSynchronize(s);
+    dfree(tmp);
+    if (e1 != hipSuccess || e2 != hipSuccess) return fail(KLSH_E_HIP, "result rows copy");
+  }
+  if (member_offsets || member_ids) {
+    std::vector<uint32_t> ord(n), head(ctx->slots), nxt(ctx->members);
+    if (n) KLSH_HIP(hipMemcpy(ord.data(), ctx->order, 4 * n, hipMemcpyDeviceToHost));
+    if (ctx->slots)
+      KLSH_HIP(hipMemcpy(head.data(), ctx->rows.head, 4 * ctx->slots, hipMemcpyDeviceToHost));
+    if (ctx->members)
+      KLSH_HIP(hipMemcpy(nxt.data(), ctx->rows.nxt, 4 * ctx->members, hipMemcpyDeviceToHost));
+    uint64_t m = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      if (member_offsets) member_offsets[i] = m;
+      for (uint32_t node = head[ord[i]]; node != klsh::kNil; node = nxt[node]) {
+        if (member_ids) member_ids[m] = ctx->ids[node];
+        ++m;
+      }
+    }
+    if (member_offsets) member_offsets[n] = m;
+  }
+  return 0;
+}
+
+int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const float* table, int h,
+                   uint32_t* keys) {
+  if (!ctx || (!rows && n) || (!keys && n) || (!table && h > 0)) return fail(KLSH_E_ARG, "null argument");
+  if (d <= 0 || d > 4096 || h < 0 || h > 31) return fail(KLSH_E_RANGE, "d or h out of range");
+  if (n >= 0xFFFFFFF0ull) return fail(KLSH_E_RANGE, "rows >= 2^32");
+  if (n == 0) return 0;
+  KLSH_HIP(hipSetDevice(ctx->device));
+  const int dp = (d + 3) & ~3;
+  Rows r{};
+  r.d = d;
+  r.dp = dp;
+  uint32_t *slots = nullptr, *dkeys = nullptr;
+  float* W = nullptr;
+  int e = 0;
+  if ((e = dalloc(&r.x, n * dp)) || (e = dalloc(&slots, n)) || (e = dalloc(&dkeys, n)) ||
+      (e = dalloc(&W, (uint64_t)std::max(h, 1) * dp))) {
+    dfree(r.x); dfree(slots); dfree(dkeys); dfree(W);
+    return e;
+  }
+  hipStream_t s = ctx->stream;
+  std::vector<uint32_t> iota(n);
+  for (uint64_t i = 0; i < n; ++i) iota[i] = (uint32_t)i;
+  int rc = 0;
+  if (hipMemsetAsync(r.x, 0, sizeof(float) * n * dp, s) != hipSuccess ||
+      hipMemcpy2DAsync(r.x, 4 * dp, rows, 4 * d, 4 * d, n, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemsetAsync(W, 0, sizeof(float) * std::max(h, 1) * dp, s) != hipSuccess ||
+      (h > 0 && hipMemcpy2DAsync(W, 4 * dp, table, 4 * d, 4 * d, h, hipMemcpyHostToDevice, s) !=
+                    hipSuccess) ||
+      hipMemcpyAsync(slots, iota.data(), 4 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+    rc = fail(KLSH_E_HIP, "upload");
+  } else {
+    klsh::launch_project(r, slots, dkeys, (uint32_t)n, W, h, 0u, s);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(keys, dkeys, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = fail(KLSH_E_HIP, "projection");
+  }
+  (void)hipStreamSynchronize(s);
+  dfree(r.x); dfree(slots); dfree(dkeys); dfree(W);
+  return rc;
+}
+
+int klsh_pcluster(klsh_ctx* ctx, float thr) {
+  if (!ctx) return fail(KLSH_E_ARG, "null ctx");
+  if (!ctx->loaded) return fail(KLSH_E_STATE, "nothing loaded");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  const uint32_t n = (uint32_t)ctx->n_live;
+  if (n == 0) return 0;
+  hipStream_t s = ctx->stream;
+  KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+  KLSH_HIP(hipMemsetAsync(ctx->keys, 0, 4ull * n, s));  // one bucket: every key equal
+  uint64_t dummy = 0;
+  return merge_and_compact(ctx, ctx->keys, ctx->order, n, thr, -1, 0, &dummy, nullptr, false);
+}
+
+int klsh_hyperplanes(uint32_t seed_base, uint64_t* rng_counter, int h, int d, float* table) {
+  if (!rng_counter || (!table && h > 0) || d <= 0 || h < 0) return fail(KLSH_E_ARG, "bad argument");
+  klsh_host_hyperplanes(seed_base, *rng_counter, (uint64_t)h, d, d, table, 1);
+  *rng_counter += (uint64_t)h;
+  return 0;
+}
+
+int klsh_fp_selftest(klsh_ctx* ctx, const float* a, const float* b, uint64_t n, float* sqrt_out,
+                     float* div_out) {
+  if (!ctx || !a || !b || !sqrt_out || !div_out) return fail(KLSH_E_ARG, "null argument");
+  if (n == 0) return 0;
+  KLSH_HIP(hipSetDevice(ctx->device));
+  float *da = nullptr, *db = nullptr, *ds = nullptr, *dd = nullptr;
+  int e = 0;
+  if ((e = dalloc(&da, n)) || (e = dalloc(&db, n)) || (e = dalloc(&ds, n)) || (e = dalloc(&dd, n))) {
+    dfree(da); dfree(db); dfree(ds); dfree(dd);
+    return e;
+  }
+  hipStream_t s = ctx->stream;
+  int rc = 0;
+  if (hipMemcpyAsync(da, a, 4 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(db, b, 4 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+    rc = fail(KLSH_E_HIP, "upload");
+  } else {
+    klsh::launch_fp_selftest(da, db, (uint32_t)n, ds, dd, s);
+    if (hipMemcpyAsync(sqrt_out, ds, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(div_out, dd, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = fail(KLSH_E_HIP, "selftest");
+  }
+  (void)hipStreamSynchronize(s);
+  dfree(da); dfree(db); dfree(ds); dfree(dd);
+  return rc;
+}
+
+}  // extern "C"

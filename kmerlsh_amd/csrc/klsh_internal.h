@@ -1,0 +1,79 @@
+// Internal interface between the host engine (klsh_engine.cpp) and the gfx950 kernels
+// (klsh_kernels.hip).  Not part of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace klsh {
+
+constexpr uint32_t kInvalid = 0xFFFFFFFFu;  // dead position marker in a bucket's slot run
+constexpr uint32_t kNil = 0xFFFFFFFFu;      // end of a member list
+constexpr int kMaxHyperplanes = 32;         // keys are uint32 (h = floor(log2 N) <= 31)
+constexpr int kSmallBucket = 32;            // buckets up to this size: one lane per bucket
+constexpr int kRadixTile = 2048;            // keys per radix-sort workgroup (256 lanes x 8 rounds)
+constexpr int kScanTile = 4096;             // items per scan workgroup (256 lanes x 16)
+
+// Device-side per-iteration counters (zeroed by the host before each iteration).
+struct Counters {
+  uint32_t n_large;  // buckets longer than kSmallBucket, queued for the wave kernel
+  uint32_t n_over;   // buckets longer than bucket_size_threshold (nestedCluster)
+  uint32_t total;    // result of the last scan/compaction (live rows)
+  uint32_t merges;   // greedy merges performed
+  uint32_t pad[4];
+};
+
+// Row state, structure-of-arrays, one entry per slot (a slot is a row of the loaded matrix;
+// a merge writes the consensus into the candidate's slot, cluster.cc:70-74).
+struct Rows {
+  float* x;        // [slots][dp] fp32 rows, dp = d rounded up to 4 (16-B aligned rows)
+  float* nrm;      // [slots] sequential sum of squares (distance.cc:33-34), cached exactly
+  uint32_t* cnt;   // [slots] member count (|_ids|)
+  uint32_t* head;  // [slots] first member node
+  uint32_t* tail;  // [slots] last member node
+  uint32_t* nxt;   // [members] next member node (kNil = end)
+  int d;
+  int dp;
+};
+
+// ---- launch wrappers (all asynchronous on `s`) ------------------------------------------------
+// keys[p] = sign-hash of row slots[p] against h hyperplanes W (h x dp), OR'ed with key_or.
+void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
+                    const float* W, int h, uint32_t key_or, hipStream_t s);
+
+// Stable LSD radix sort of (keys, vals)[0..n) on the low `bits` bits. Uses ping-pong buffers;
+// returns via *out_k/*out_v which pair holds the result (one of (k0,v0) or (k1,v1)).
+void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
+                uint32_t* hist, uint32_t* tile_sums, Counters* ctr, uint32_t** out_k,
+                uint32_t** out_v, hipStream_t s);
+
+// Greedy merge over bucket runs of equal key in positions [lo, hi) of (key, slots).
+// Small runs: one lane each; longer runs are queued and done one wave each.  Runs longer than
+// bucket_thr (>= 0) are queued to `over` (p, len) and left untouched.
+void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
+                  float thr, int bucket_thr, uint32_t* large_list, uint2* over_list, Counters* ctr,
+                  hipStream_t s);
+
+// out[0..total) = slots[p] for p with slots[p] != kInvalid, stable; ctr->total = count.
+void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
+                    Counters* ctr, hipStream_t s);
+
+// Mode-C producer: rows x[i] (slot i) from counts (d x bs, sample-major), LUT ln(c+1),
+// v_kmers; order[] = kept rows (sum > 0.1 d) compacted; ctr->total = kept count.
+void launch_convert(const Rows& r, const uint16_t* counts, uint32_t bs, const float* lut,
+                    const float* v_kmers, uint32_t* keep, uint32_t* order, uint32_t* tile_sums,
+                    Counters* ctr, hipStream_t s);
+
+// Sequential norms nrm[slot] for slots [0, n) (after a load).
+void launch_norms(const Rows& r, uint32_t n, hipStream_t s);
+
+// out[i*d + k] = x[order[i]][k] (compact result rows).
+void launch_gather_rows(const Rows& r, const uint32_t* order, uint32_t n, float* out,
+                        hipStream_t s);
+
+// Floating-point self test: sqrt_out[i] = sqrtf(a[i]); div_out[i] = a[i] / b[i] as the merge
+// kernels evaluate them.
+void launch_fp_selftest(const float* a, const float* b, uint32_t n, float* sqrt_out,
+                        float* div_out, hipStream_t s);
+
+}  // namespace klsh

@@ -379,6 +379,11 @@ int klsh_oracle_cluster(klsh_oracle_state* st, float min_similarity, int iters,
   return it;
 }
 
+uint64_t klsh_oracle_pcluster(klsh_oracle_state* st, float threshold) {
+  st->n = p_cluster(st, st->order, st->n, threshold);
+  return st->n;
+}
+
 void klsh_oracle_result(const klsh_oracle_state* st, float* rows, uint64_t* member_offsets,
                         uint64_t* member_ids) {
   const int d = st->d;

@@ -62,6 +62,10 @@ int klsh_oracle_cluster(klsh_oracle_state* st, float min_similarity, int iters,
                         int bucket_size_threshold, klsh_oracle_rng* rng, uint64_t* nt_trace,
                         int nthreads);
 
+/* p_cluster (reference function/cluster.cc:56-87) over the live rows taken as ONE bucket in
+ * their current order; survivors become the live rows.  Returns the survivor count. */
+uint64_t klsh_oracle_pcluster(klsh_oracle_state* st, float threshold);
+
 /* Output in canonical order: rows (count*d), member_offsets (count+1), member_ids (members). */
 void klsh_oracle_result(const klsh_oracle_state* st, float* rows, uint64_t* member_offsets,
                         uint64_t* member_ids);

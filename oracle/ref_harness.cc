@@ -71,6 +71,7 @@ int main(int argc, char** argv) {
             "  ref_harness consensus ROWS D CA CB OUT       (SetConsensus of row0 (CA ids) and row1 (CB ids))\n"
             "  ref_harness cluster ROWS N D MINSIM I BTHR OUTPREFIX\n"
             "  ref_harness cluster_from BINPREFIX D MINSIM I BTHR OUTPREFIX   (input via ReadClusterAll)\n"
+            "  ref_harness cluster_w ROWS OFF IDS N D MINSIM I BTHR OUTPREFIX (binary member lists)\n"
             "  ref_harness convert COUNTS N D VKMERS OUTPREFIX  (uint16 sample-major counts -> convertHTMat)\n");
     return 1;
   }
@@ -138,11 +139,31 @@ int main(int argc, char** argv) {
     write_bytes(argv[6], c._values.data(), (size_t)d * 4);
     return 0;
   }
-  if (cmd == "cluster" || cmd == "cluster_from") {
+  if (cmd == "cluster" || cmd == "cluster_from" || cmd == "cluster_w") {
     vector<Abundance*> v;
     int argi;
     int d;
-    if (cmd == "cluster") {
+    if (cmd == "cluster_w") {  // ROWS.f32 OFF.u64 IDS.u64 N D ...: rows with member-id lists
+      const size_t n = strtoull(argv[5], nullptr, 10);
+      d = atoi(argv[6]);
+      vector<float> x = read_f32(argv[2], n * d);
+      vector<uint64_t> off(n + 1);
+      FILE* f = fopen(argv[3], "rb");
+      if (!f || fread(off.data(), 8, n + 1, f) != n + 1) { fprintf(stderr, "read off\n"); return 2; }
+      fclose(f);
+      vector<uint64_t> ids(off[n]);
+      f = fopen(argv[4], "rb");
+      if (!f || (off[n] && fread(ids.data(), 8, off[n], f) != off[n])) { fprintf(stderr, "read ids\n"); return 2; }
+      fclose(f);
+      v.reserve(n);
+      for (size_t i = 0; i < n; ++i) {
+        Abundance* a = new Abundance();
+        a->_values.assign(x.begin() + i * d, x.begin() + (i + 1) * d);
+        a->_ids.assign(ids.begin() + off[i], ids.begin() + off[i + 1]);
+        v.push_back(a);
+      }
+      argi = 7;
+    } else if (cmd == "cluster") {
       const size_t n = strtoull(argv[3], nullptr, 10);
       d = atoi(argv[4]);
       vector<float> x = read_f32(argv[2], n * d);

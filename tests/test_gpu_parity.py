@@ -1,0 +1,225 @@
+"""Parity of the gfx950 engine (through the C ABI) with the reference and the oracle.
+
+Bar: bit-exact.  Keys, survivor order, member-id lists, N_t traces and the fp32 centroid bits
+must all equal the reference's outputs (golden fixtures made by the reference itself) and the
+oracle's on the same seeded inputs; at full size, size-independent properties are checked.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, golden
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, GOLDEN)
+
+
+def same_bits(a, b):
+    return np.array_equal(np.ascontiguousarray(a, np.float32).view(np.uint32),
+                          np.ascontiguousarray(b, np.float32).view(np.uint32))
+
+
+def assert_same_result(got, rows, off, ids):
+    g_rows, g_off, g_ids = got
+    assert np.array_equal(g_off, off)
+    assert np.array_equal(g_ids, ids)
+    assert same_bits(g_rows, rows)
+
+
+# --------------------------------------------------------------------------- arithmetic ------
+def test_fp_sqrt_div_correctly_rounded(engine):
+    rng = np.random.default_rng(1)
+    a = np.concatenate([rng.random(200000).astype(np.float32) * 1e4,
+                        rng.random(20000).astype(np.float32) * np.float32(1e-38),  # subnormal
+                        np.array([0, 1, 2, 3, 4, 1e30, 3.4e38], np.float32)])
+    b = np.concatenate([rng.random(a.size - 7).astype(np.float32) * 100 + 1e-3,
+                        np.array([1, 3, 7, 0.1, 9, 1e-30, 0.5], np.float32)])
+    s, q = engine.fp_selftest(a, b)
+    assert same_bits(s, np.sqrt(a))
+    assert same_bits(q, a / b)
+
+
+@pytest.mark.parametrize("name", ["keys_d8", "keys_d16", "keys_d64", "keys_d13", "keys_d512"])
+def test_hash_keys_match_reference(engine, name):
+    from kmerlsh_amd import _native
+
+    z = golden(name + ".npz")
+    w, _ = _native.hyperplanes(int(z["seed"]), 0, int(z["h"]), z["rows"].shape[1])
+    assert np.array_equal(engine.hash_keys(z["rows"], w), z["keys"])
+
+
+def test_hash_keys_random_vs_oracle(engine, oracle):
+    from kmerlsh_amd import _native
+
+    rng = np.random.default_rng(3)
+    for d, h in [(32, 17), (64, 31), (8, 1), (5, 7), (100, 20)]:
+        rows = rng.normal(0, 1, size=(3000, d)).astype(np.float32)
+        w, _ = _native.hyperplanes(99 + d, 5, h, d)
+        assert np.array_equal(engine.hash_keys(rows, w), oracle.keys(rows, w)), (d, h)
+
+
+# ------------------------------------------------------------------------------ p_cluster ---
+@pytest.mark.parametrize("name", ["pcluster_small", "pcluster_large", "pcluster_generic",
+                                  "pcluster_d8"])
+def test_pcluster_matches_reference(engine, name):
+    z = golden(name + ".npz")
+    engine.load_rows(z["rows"])
+    engine.pcluster(float(z["thr"]))
+    assert_same_result(engine.result(), z["out_rows"], z["out_off"], z["out_ids"])
+
+
+@pytest.mark.parametrize("b,d", [(33, 64), (1000, 16), (5000, 8)])
+def test_pcluster_identical_rows(engine, oracle, b, d):
+    """Degenerate bucket (every row identical): the wave kernel merges i into j = 0 each step."""
+    rows = np.tile(np.linspace(-1, 2, d, dtype=np.float32), (b, 1))
+    engine.load_rows(rows)
+    engine.pcluster(0.95)
+    assert_same_result(engine.result(), *oracle.pcluster(rows, 0.95))
+
+
+# ------------------------------------------------------------------------------- Cluster ----
+CLUSTER_CASES = ["cluster_d16", "cluster_d64", "cluster_d12", "cluster_d8_init", "cluster_nested",
+                 "cluster_nested_small"]
+
+
+@pytest.mark.parametrize("name", CLUSTER_CASES)
+def test_cluster_matches_reference(engine, name):
+    z = golden(name + ".npz")
+    engine.load_rows(z["rows"])
+    trace, counter, stats = engine.cluster(float(z["min_sim"]), int(z["iters"]), int(z["bthr"]),
+                                           int(z["seed"]), 0)
+    assert np.array_equal(trace, z["trace"])
+    assert_same_result(engine.result(), z["out_rows"], z["out_off"], z["out_ids"])
+
+
+def test_cluster_weighted_matches_reference(engine):
+    z = golden("cluster_weighted.npz")
+    engine.load_rows(z["rows"], z["in_off"], z["in_ids"])
+    trace, _, _ = engine.cluster(float(z["min_sim"]), int(z["iters"]), int(z["bthr"]),
+                                 int(z["seed"]), 0)
+    assert np.array_equal(trace, z["trace"])
+    assert_same_result(engine.result(), z["out_rows"], z["out_off"], z["out_ids"])
+
+
+def test_convert_matches_reference(engine):
+    z = golden("convert.npz")
+    engine.load_counts(z["counts"], z["v_kmers"])
+    rows, off, ids = engine.result()
+    assert np.array_equal(ids, z["out_ids"])
+    assert np.array_equal(np.diff(off), np.ones(len(ids), np.uint64))
+    assert same_bits(rows, z["out_rows"])
+
+
+def clustered(rng, n, d, groups, noise):
+    centers = rng.normal(0, 1, size=(groups, d)).astype(np.float32)
+    return (centers[rng.integers(0, groups, n)] +
+            rng.normal(0, noise, size=(n, d)).astype(np.float32)).astype(np.float32)
+
+
+@pytest.mark.parametrize("n,d,groups,iters,bthr", [
+    (200000, 64, 4000, 12, 1000000),
+    (100000, 32, 500, 8, 1000000),
+    (60000, 20, 300, 6, 1000000),      # generic kernels
+    (50000, 16, 3, 3, 5000),           # nested path in every iteration
+])
+def test_cluster_random_vs_oracle(engine, oracle, n, d, groups, iters, bthr):
+    rng = np.random.default_rng(n + d)
+    rows = clustered(rng, n, d, groups, 0.05)
+    engine.load_rows(rows)
+    trace, counter, _ = engine.cluster(0.8, iters, bthr, 777, 3)
+    o_rows, o_off, o_ids, o_trace, o_counter = oracle.cluster(rows, 0.8, iters, bthr, 777, 3)
+    assert np.array_equal(trace, o_trace)
+    assert counter == o_counter
+    assert_same_result(engine.result(), o_rows, o_off, o_ids)
+
+
+def test_cluster_repeat_and_restore_deterministic(engine):
+    rng = np.random.default_rng(5)
+    rows = clustered(rng, 100000, 64, 2000, 0.05)
+    engine.load_rows(rows)
+    engine.snapshot()
+    engine.cluster(0.8, 10, 1000000, 1, 0)
+    a = engine.result()
+    engine.restore()
+    engine.cluster(0.8, 10, 1000000, 1, 0)
+    b = engine.result()
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_empty_and_single(engine):
+    engine.load_rows(np.zeros((0, 8), np.float32))
+    trace, counter, _ = engine.cluster(0.8, 3, 10, 1, 0)
+    assert list(trace) == [0, 0, 0] and counter == 0
+    engine.load_rows(np.ones((1, 8), np.float32))
+    trace, counter, _ = engine.cluster(0.8, 3, 10, 1, 0)
+    assert list(trace) == [1, 1, 1] and counter == 0
+
+
+# ------------------------------------------------------------------- mode C, end to end ------
+@pytest.mark.parametrize("kat", ["katF", "katG", "katN"])
+def test_cli_kat_md5(kat, tmp_path):
+    import kat_inputs
+    from kmerlsh_amd import _native
+
+    with open(os.path.join(GOLDEN, "kat_md5.json")) as f:
+        ref = json.load(f)[kat]
+    kat_inputs.write_kat(kat, str(tmp_path))
+    out = subprocess.run([_native.CLI_PATH, "-a", "a.txt", "-b", "b.txt", "-I", "10", "-M", "C",
+                          "--only", "--seed", "12345", "--verbose"], cwd=tmp_path, check=True,
+                         capture_output=True, text=True, timeout=300).stdout
+    for fn, md5 in ref["md5"].items():
+        with open(tmp_path / fn, "rb") as f:
+            assert hashlib.md5(f.read()).hexdigest() == md5, fn
+    trace = [int(line.split(":")[1]) for line in out.splitlines() if line.startswith("Size of")]
+    assert trace == ref["trace"]
+
+
+def test_synth_mode_c_vs_oracle(engine, oracle):
+    """klsh-synth counts -> GPU convert -> init pass -> main loop, against the oracle."""
+    from kmerlsh_amd import _native
+
+    n, d = 400000, 32
+    counts, cov = _native.synth_counts(n, d, seed=13)
+    v_kmers = (cov.astype(np.float32) / np.float32(n)).astype(np.float32)
+    engine.load_counts(counts, v_kmers)
+    t0, c0, _ = engine.cluster(0.8, 1, 100000, 12345, 0)
+    t1, c1, _ = engine.cluster(0.8, 10, 1000000, 12345, c0)
+    got = engine.result()
+    rows, ids = oracle.convert(counts, v_kmers)
+    r1, o1, i1, tr0, k0 = oracle.cluster(rows, 0.8, 1, 100000, 12345, 0, None, ids)
+    r2, o2, i2, tr1, k1 = oracle.cluster(r1, 0.8, 10, 1000000, 12345, k0, o1, i1)
+    assert np.array_equal(t0, tr0) and np.array_equal(t1, tr1) and c1 == k1
+    assert_same_result(got, r2, o2, i2)
+
+
+def test_full_size_c2_properties(engine):
+    """C2 shape (10M x 64): size-independent properties of the GPU result (the oracle is
+    too slow at this size for every test run; bench.py compares a bounded sample)."""
+    from kmerlsh_amd import _native
+
+    n, d = 10_000_000, 64
+    counts, cov = _native.synth_counts(n, d, seed=11)
+    v_kmers = (cov.astype(np.float32) / np.float32(n)).astype(np.float32)
+    engine.load_counts(counts, v_kmers)
+    del counts
+    n_kept, _ = engine.count()
+    _, c0, _ = engine.cluster(0.8, 1, 100000, 12345, 0)
+    engine.snapshot()
+    trace, c1, st = engine.cluster(0.8, 20, 1000000, 12345, c0)
+    rows, off, ids = engine.result()
+    assert np.all(np.diff(trace.astype(np.int64)) <= 0)          # N_t never grows
+    assert int(off[-1]) == n_kept                                 # members partition the rows
+    assert np.array_equal(np.sort(ids), np.unique(ids)) and ids.size == n_kept
+    assert np.all(np.isfinite(rows))
+    engine.restore()                                              # replay: identical
+    trace2, c2, _ = engine.cluster(0.8, 20, 1000000, 12345, c0)
+    rows2, off2, ids2 = engine.result()
+    assert np.array_equal(trace, trace2) and c1 == c2
+    assert np.array_equal(off, off2) and np.array_equal(ids, ids2) and same_bits(rows, rows2)

@@ -1,0 +1,67 @@
+"""Static checks of the gfx950 code object (CPU only: hipcc cross-compiles).
+
+The reference never fuses multiply-add, so the sign-hash kernels must contain
+no v_fma*/v_fmac*/v_pk_fma*/v_mad_f32 at all, and the dot products of the merge kernels must use
+separate v_mul/v_add.  sqrt and division must be the correctly rounded expansions (those use
+FMA-based refinement internally, which is exact by construction).
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+CSRC = os.path.join(ROOT, "kmerlsh_amd", "csrc")
+ASM = os.path.join(ROOT, "kmerlsh_amd", "build", "klsh_kernels.s")
+FMA = re.compile(r"^\s+(v_fma\w*|v_fmac\w*|v_pk_fma\w*|v_mad_f32\w*|v_fmamk\w*|v_fmaak\w*)\b")
+
+
+@pytest.fixture(scope="module")
+def kernels():
+    subprocess.run(["make", "-s", "-C", CSRC, "isa"], check=True)
+    text = open(ASM).read()
+    out = {}
+    for m in re.finditer(r"^(_Z\w+):[^\n]*\n(.*?)^\.Lfunc_end", text, re.M | re.S):
+        out[m.group(1)] = m.group(2)
+    assert out, "no kernels found in the assembly"
+    return out
+
+
+def test_target_is_gfx950(kernels):
+    text = open(ASM).read()
+    assert "gfx950" in text
+
+
+def test_projection_has_no_fused_multiply_add(kernels):
+    proj = {k: v for k, v in kernels.items() if "k_project" in k}
+    assert len(proj) == 5  # d = 8, 16, 32, 64 and the generic kernel
+    for name, body in proj.items():
+        bad = [ln.strip() for ln in body.splitlines() if FMA.match(ln)]
+        assert not bad, (name, bad[:5])
+        assert "v_mul_f32" in body or "v_pk_mul_f32" in body
+        assert "v_add_f32" in body
+
+
+def test_merge_dot_products_are_unfused(kernels):
+    """In the merge kernels every FMA must belong to a sqrt/div expansion: their count per kernel
+    is bounded by the number of sqrt/div sequences, while the dot products (d multiplies + adds
+    per pair) appear as v_mul/v_add."""
+    merge = {k: v for k, v in kernels.items() if "k_merge" in k}
+    assert merge
+    for name, body in merge.items():
+        n_fma = sum(1 for ln in body.splitlines() if FMA.match(ln))
+        n_div = body.count("v_div_fixup_f32")
+        n_sqrt = body.count("v_sqrt_f32")
+        # correctly rounded f32 division = 1 rcp + 5 fma-class ops + fmas + fixup; sqrt
+        # refinement <= 4 fma-class ops
+        assert n_fma <= 6 * n_div + 4 * n_sqrt, (name, n_fma, n_div, n_sqrt)
+        assert n_div >= 1 and n_sqrt >= 1, name
+        assert "v_add_f32" in body
+
+
+def test_correctly_rounded_division_and_sqrt(kernels):
+    body = kernels[next(k for k in kernels if "k_fp_selftest" in k)]
+    assert "v_div_scale_f32" in body and "v_div_fixup_f32" in body
+    assert "v_sqrt_f32" in body
