@@ -1,0 +1,214 @@
+// Device helpers shared by the gfx950 kernels (klsh_kernels.hip, klsh_merge.hip).
+// Numerics contract: see klsh_kernels.hip (sequential fp32, no FMA, IEEE sqrt/div).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "klsh_internal.h"
+
+namespace klsh {
+
+// ============================================================================ helpers ==========
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// The merge test of cluster.cc:68-69 given the exact sequential dot product and the cached
+// sequential norms: sim = dot / (sqrtf(|a|^2) * sqrtf(|b|^2)); dist = 1 - sim; 1 - dist >= thr.
+__device__ __forceinline__ bool cos_decide(float dot, float ni, float nj, float thr) {
+  const float den = __builtin_sqrtf(ni) * __builtin_sqrtf(nj);
+  const float sim = dot / den;
+  const float dist = 1.0f - sim;
+  return (1.0f - dist) >= thr;
+}
+
+// Consensus element (funcAB.cc:65): v1*c1/n + v2*c2/n, each op rounded, current row first.
+__device__ __forceinline__ float consensus(float cur, float fa, float cand, float fb, float fn) {
+  const float a = (cur * fa) / fn;
+  const float b = (cand * fb) / fn;
+  return a + b;
+}
+
+template <int D>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, float (&x)[D]) {
+#pragma unroll
+  for (int k = 0; k < D; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p + k);
+    x[k] = v.x;
+    x[k + 1] = v.y;
+    x[k + 2] = v.z;
+    x[k + 3] = v.w;
+  }
+}
+
+template <int D>
+__device__ __forceinline__ float dot_reg_mem(const float (&a)[D], const float* __restrict__ b) {
+  float s = 0.0f;
+#pragma unroll
+  for (int k = 0; k < D; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(b + k);
+    s = s + a[k] * v.x;
+    s = s + a[k + 1] * v.y;
+    s = s + a[k + 2] * v.z;
+    s = s + a[k + 3] * v.w;
+  }
+  return s;
+}
+
+__device__ __forceinline__ float dot_mem_mem(const float* a, const float* b, int d) {
+  float s = 0.0f;
+  for (int k = 0; k < d; ++k) s = s + a[k] * b[k];
+  return s;
+}
+
+__device__ __forceinline__ float norm_mem(const float* a, int d) {
+  float s = 0.0f;
+  for (int k = 0; k < d; ++k) s = s + a[k] * a[k];
+  return s;
+}
+
+// Member list of `cur` goes in front of `cand`'s (funcAB.cc:51-55: ids = ids_cur ++ ids_cand).
+__device__ __forceinline__ void link_members(const Rows& r, uint32_t cur, uint32_t cand) {
+  const uint32_t ca = r.cnt[cur], cb = r.cnt[cand];
+  r.nxt[r.tail[cur]] = r.head[cand];
+  r.head[cand] = r.head[cur];
+  r.cnt[cand] = ca + cb;
+  r.cnt[cur] = 0;
+}
+
+// =============================================================================== scans ==========
+// 256-lane exclusive scan; returns the lane's exclusive prefix, *total = block sum.
+__device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t wsum[5];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t t = wsum[i];
+      wsum[i] = a;
+      a += t;
+    }
+    wsum[4] = a;
+  }
+  __syncthreads();
+  const uint32_t r = x - v + wsum[w];
+  *total = wsum[4];
+  __syncthreads();
+  return r;
+}
+
+struct SrcArray {
+  const uint32_t* a;
+  __device__ uint32_t operator()(uint32_t i) const { return a[i]; }
+};
+struct DstExclusive {  // in-place exclusive prefix
+  uint32_t* a;
+  __device__ void operator()(uint32_t i, uint32_t prefix, uint32_t) const { a[i] = prefix; }
+};
+struct SrcLive {
+  const uint32_t* s;
+  __device__ uint32_t operator()(uint32_t i) const { return s[i] != kInvalid ? 1u : 0u; }
+};
+struct DstCompact {
+  const uint32_t* s;
+  uint32_t* out;
+  __device__ void operator()(uint32_t i, uint32_t prefix, uint32_t v) const {
+    if (v) out[prefix] = s[i];
+  }
+};
+struct DstCompactIndex {  // out[prefix] = i for kept i
+  uint32_t* out;
+  __device__ void operator()(uint32_t i, uint32_t prefix, uint32_t v) const {
+    if (v) out[prefix] = i;
+  }
+};
+
+template <class Src>
+__global__ __launch_bounds__(256) void k_scan_tile_sum(Src src, uint32_t n, uint32_t* tile_sums) {
+  const uint32_t base = blockIdx.x * (uint32_t)kScanTile + threadIdx.x * 16u;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (base + k < n) acc += src(base + k);
+  uint32_t total;
+  block_excl_scan_256(acc, &total);
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+// One workgroup of 1024 lanes scans the tile sums in place (exclusive); *total = grand total.
+template <int kUnused = 0>
+__global__ __launch_bounds__(1024) void k_scan_tiles(uint32_t* tile_sums, uint32_t ntiles,
+                                                     uint32_t* total) {
+  __shared__ uint32_t wsum[17];
+  __shared__ uint32_t carry;
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c = 0; c < ntiles; c += 1024) {
+    const uint32_t i = c + threadIdx.x;
+    const uint32_t v = i < ntiles ? tile_sums[i] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t a = 0;
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t t = wsum[k];
+        wsum[k] = a;
+        a += t;
+      }
+      wsum[16] = a;
+    }
+    __syncthreads();
+    if (i < ntiles) tile_sums[i] = carry + wsum[w] + x - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += wsum[16];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+template <class Src, class Dst>
+__global__ __launch_bounds__(256) void k_scan_apply(Src src, Dst dst, uint32_t n,
+                                                    const uint32_t* __restrict__ tile_sums) {
+  const uint32_t base = blockIdx.x * (uint32_t)kScanTile + threadIdx.x * 16u;
+  uint32_t v[16];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = (base + k < n) ? src(base + k) : 0u;
+    acc += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan_256(acc, &total) + tile_sums[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (base + k < n) dst(base + k, run, v[k]);
+    run += v[k];
+  }
+}
+
+template <class Src, class Dst>
+inline void device_scan(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, uint32_t* total,
+                        hipStream_t s) {
+  const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
+  if (ntiles == 0) {
+    (void)hipMemsetAsync(total, 0, sizeof(uint32_t), s);
+    return;
+  }
+  k_scan_tile_sum<Src><<<ntiles, 256, 0, s>>>(src, n, tile_sums);
+  k_scan_tiles<0><<<1, 1024, 0, s>>>(tile_sums, ntiles, total);
+  k_scan_apply<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, tile_sums);
+}
+
+}  // namespace klsh

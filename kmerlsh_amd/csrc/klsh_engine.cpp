@@ -14,6 +14,9 @@
 // ascending bucket order (the reference's T=1 RNG order), sorted, merged, and 5 is redone.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <stddef.h>
 #include <string.h>
 
 #include <algorithm>
@@ -108,8 +111,7 @@ struct klsh_ctx {
   uint32_t* nv2 = nullptr;
   uint32_t* hist = nullptr;
   uint32_t* tile_sums = nullptr;
-  uint32_t* large_list = nullptr;
-  uint2* over_list = nullptr;
+  klsh::MergeWork mw{};
   Counters* ctr = nullptr;
   Counters* h_ctr = nullptr;  // pinned
   float* W = nullptr;         // hyperplane pool on the device, [k - w_k0][dp]
@@ -126,7 +128,8 @@ struct klsh_ctx {
   void release_state() {
     dfree(rows.x); dfree(rows.nrm); dfree(rows.cnt); dfree(rows.head); dfree(rows.tail);
     dfree(rows.nxt); dfree(order); dfree(alt); dfree(keys); dfree(keys2); dfree(nk1);
-    dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(large_list); dfree(over_list);
+    dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.seg); dfree(mw.over);
+    dfree(mw.big); dfree(mw.huge);
     cap_slots = cap_members = 0;
     cap_dp = 0;
     drop_snapshot();
@@ -171,11 +174,12 @@ struct klsh_ctx {
         (e = dalloc(&nv2, s)) ||
         (e = dalloc(&hist, 256 * ((s + klsh::kRadixTile - 1) / klsh::kRadixTile) + 256)) ||
         (e = dalloc(&tile_sums, (256 * s) / klsh::kScanTile + 1024)) ||
-        (e = dalloc(&large_list, s / (klsh::kSmallBucket + 1) + 64)) ||
-        (e = dalloc(&over_list, s + 64))) {
+        (e = dalloc(&mw.seg, s + 64)) || (e = dalloc(&mw.over, s + 64)) ||
+        (e = dalloc(&mw.big, s / 65 + 64)) || (e = dalloc(&mw.huge, s / (klsh::kBigRows + 1) + 64))) {
       release_state();
       return e;
     }
+    mw.tile_sums = tile_sums;
     cap_slots = s;
     cap_members = m;
     cap_dp = dp_;
@@ -454,8 +458,7 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
   hipStream_t s = ctx->stream;
   uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
-  klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->large_list, ctx->over_list,
-                     ctx->ctr, s);
+  klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->mw, ctx->ctr, s);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[3], s));
   klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
@@ -470,7 +473,7 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
   if (n_over > 0) {
     // nestedCluster (cluster.cc:286-288 -> :89-178) for each oversize bucket, ascending.
     std::vector<uint2> over(n_over);
-    KLSH_HIP(hipMemcpy(over.data(), ctx->over_list, sizeof(uint2) * n_over, hipMemcpyDeviceToHost));
+    KLSH_HIP(hipMemcpy(over.data(), ctx->mw.over, sizeof(uint2) * n_over, hipMemcpyDeviceToHost));
     std::sort(over.begin(), over.end(), [](const uint2& a, const uint2& b) { return a.x < b.x; });
     for (uint32_t oi = 0; oi < n_over; ++oi) {
       const uint32_t p = over[oi].x, b = over[oi].y;
@@ -492,9 +495,10 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
                        ctx->ctr, &rk, &rv, s);
       KLSH_HIP(hipMemcpyAsync(fk + p, rk, 4ull * b, hipMemcpyDeviceToDevice, s));
       if (rv != fv + p) KLSH_HIP(hipMemcpyAsync(fv + p, rv, 4ull * b, hipMemcpyDeviceToDevice, s));
-      KLSH_HIP(hipMemsetAsync(&ctx->ctr->n_large, 0, sizeof(uint32_t), s));
-      klsh::launch_merge(ctx->rows, fk, fv, p, p + b, thr, -1, ctx->large_list, ctx->over_list,
-                         ctx->ctr, s);
+      // fresh run lists for the region (n_seg .. n_over are contiguous)
+      KLSH_HIP(hipMemsetAsync(&ctx->ctr->n_seg, 0,
+                              offsetof(Counters, total) - offsetof(Counters, n_seg), s));
+      klsh::launch_merge(ctx->rows, fk, fv, p, p + b, thr, -1, ctx->mw, ctx->ctr, s);
       KLSH_HIP(hipGetLastError());
     }
     klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
@@ -534,6 +538,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   for (; it < iterations; ++it) {
     const uint64_t n = ctx->n_live;
     if (nt_trace) nt_trace[it] = n;
+    st->iterations += 1;
     if (n == 0) {  // the reference aborts here (cluster.cc:194 on an empty vector); no-op
       threshold -= sim_step;
       continue;
@@ -555,13 +560,39 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
                      ctx->tile_sums, ctx->ctr, &fk, &fv, s);
     KLSH_HIP(hipGetLastError());
     KLSH_HIP(hipEventRecord(ctx->ev[5], s));
+    if (const char* path = getenv("KLSH_BUCKET_STATS")) {  // diagnostics: run-length histogram
+      std::vector<uint32_t> hk(n);
+      KLSH_HIP(hipMemcpyAsync(hk.data(), fk, 4 * n, hipMemcpyDeviceToHost, s));
+      KLSH_HIP(hipStreamSynchronize(s));
+      uint64_t hist[12] = {0}, pairs = 0, maxb = 0, rows_in[12] = {0};
+      for (uint64_t a = 0; a < n;) {
+        uint64_t b = a + 1;
+        while (b < n && hk[b] == hk[a]) ++b;
+        const uint64_t len = b - a;
+        int c = 0;
+        while (c < 11 && (1ull << c) < len) ++c;  // class c: len in (2^(c-1), 2^c]
+        hist[c]++;
+        rows_in[c] += len;
+        pairs += len * (len - 1) / 2;
+        maxb = std::max(maxb, len);
+        a = b;
+      }
+      if (FILE* f = fopen(path, "a")) {
+        fprintf(f, "{\"it\": %d, \"n\": %llu, \"h\": %d, \"pairs\": %llu, \"max\": %llu, \"hist\": [", it,
+                (unsigned long long)n, h, (unsigned long long)pairs, (unsigned long long)maxb);
+        for (int c = 0; c < 12; ++c) fprintf(f, "%s%llu", c ? ", " : "", (unsigned long long)hist[c]);
+        fprintf(f, "], \"rows\": [");
+        for (int c = 0; c < 12; ++c) fprintf(f, "%s%llu", c ? ", " : "", (unsigned long long)rows_in[c]);
+        fprintf(f, "]}\n");
+        fclose(f);
+      }
+    }
     if (int e = merge_and_compact(ctx, fk, fv, (uint32_t)n, threshold, bucket_size_threshold,
                                   seed_base, rng_counter, st, true))
       return e;
     st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
     st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
     st->project_launches += 1;
-    st->iterations += 1;
     st->sum_rows += n;
     st->sum_proj_bits += n * (uint64_t)h;
     st->sum_merges += n - ctx->n_live;

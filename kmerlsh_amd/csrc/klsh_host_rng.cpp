@@ -12,6 +12,19 @@
 #include <thread>
 #include <vector>
 
+#include <cstdlib>
+
+
+// Host worker threads: OMP_NUM_THREADS if set (the GPU boxes set it to their CPU share), else
+// min(16, hardware threads).
+static int klsh_default_threads() {
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int v = std::atoi(e);
+    if (v > 0) return v;
+  }
+  return (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+}
+
 extern "C" {
 
 uint32_t klsh_host_seed(uint32_t base, uint64_t k) { return base + (uint32_t)k * 2654435761u; }
@@ -26,7 +39,7 @@ void klsh_host_hyperplane(uint32_t seed, int d, float* out) {
 void klsh_host_hyperplanes(uint32_t base, uint64_t k0, uint64_t count, int d, int stride,
                            float* out, int threads) {
   if (count == 0) return;
-  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (threads <= 0) threads = klsh_default_threads();
   const uint64_t per = 8;  // hyperplanes per work item
   const uint64_t items = (count + per - 1) / per;
   const int nt = (int)std::min<uint64_t>((uint64_t)threads, items);

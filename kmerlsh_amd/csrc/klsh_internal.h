@@ -10,17 +10,31 @@ namespace klsh {
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;  // dead position marker in a bucket's slot run
 constexpr uint32_t kNil = 0xFFFFFFFFu;      // end of a member list
 constexpr int kMaxHyperplanes = 32;         // keys are uint32 (h = floor(log2 N) <= 31)
-constexpr int kSmallBucket = 32;            // buckets up to this size: one lane per bucket
 constexpr int kRadixTile = 2048;            // keys per radix-sort workgroup (256 lanes x 8 rounds)
 constexpr int kScanTile = 4096;             // items per scan workgroup (256 lanes x 16)
 
+// Bucket runs longer than 64 rows and up to kBigRows rows are merged by one workgroup with the
+// run in LDS (k_merge_big); longer runs by one wave from memory (k_merge_wave).
+constexpr int kBigRows = 384;
+constexpr int kBigWords = kBigRows / 64;
+
 // Device-side per-iteration counters (zeroed by the host before each iteration).
 struct Counters {
-  uint32_t n_large;  // buckets longer than kSmallBucket, queued for the wave kernel
-  uint32_t n_over;   // buckets longer than bucket_size_threshold (nestedCluster)
-  uint32_t total;    // result of the last scan/compaction (live rows)
-  uint32_t merges;   // greedy merges performed
-  uint32_t pad[4];
+  uint32_t n_seg;   // bucket runs found by the segment scan
+  uint32_t n_big;   // runs of 65..kBigRows rows queued for k_merge_big
+  uint32_t n_huge;  // runs longer than kBigRows queued for k_merge_wave
+  uint32_t n_over;  // runs longer than bucket_size_threshold (nestedCluster)
+  uint32_t total;   // result of the last scan/compaction (live rows)
+  uint32_t pad[11];
+};
+
+// Merge workspace (device), sized for `cap` positions.
+struct MergeWork {
+  uint32_t* seg;   // run starts [n_seg]
+  uint2* big;      // (start, length) of runs for k_merge_big
+  uint2* huge;     // (start, length) of runs for k_merge_wave
+  uint2* over;     // (start, length) of oversize runs
+  uint32_t* tile_sums;
 };
 
 // Row state, structure-of-arrays, one entry per slot (a slot is a row of the loaded matrix;
@@ -47,12 +61,11 @@ void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t
                 uint32_t* hist, uint32_t* tile_sums, Counters* ctr, uint32_t** out_k,
                 uint32_t** out_v, hipStream_t s);
 
-// Greedy merge over bucket runs of equal key in positions [lo, hi) of (key, slots).
-// Small runs: one lane each; longer runs are queued and done one wave each.  Runs longer than
-// bucket_thr (>= 0) are queued to `over` (p, len) and left untouched.
+// Greedy merge (p_cluster) over every bucket run of equal key in positions [lo, hi) of
+// (key, slots), in place: survivors first in each run, kInvalid after.  Runs longer than
+// bucket_thr (>= 0) are queued to w.over (start, length) and left untouched.
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
-                  float thr, int bucket_thr, uint32_t* large_list, uint2* over_list, Counters* ctr,
-                  hipStream_t s);
+                  float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s);
 
 // out[0..total) = slots[p] for p with slots[p] != kInvalid, stable; ctr->total = count.
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,

@@ -1,0 +1,631 @@
+// Greedy in-bucket merge for gfx950: p_cluster (reference function/cluster.cc:56-87) with the
+// cosine test (function/distance.cc:27-38) and the consensus (function/funcAB.cc:49-71), run
+// over every bucket of one LSH iteration.
+//
+// The reference walks a bucket sequentially: row i merges into the FIRST j < i with
+// 1 - cosine(i, j) >= thr; the consensus replaces j, row i is overwritten by the last row and
+// re-tested.  A decision only changes when one of its two rows changes, and only the candidate j
+// of a merge changes, so the GPU version evaluates decisions in bulk and replays the walk:
+//
+//   segment scan    bucket runs = positions where the sorted key changes (parallel scan)
+//   k_merge_window  one wave per window of 64 runs.  Runs of 2..64 rows are handled in place by
+//                   G-lane groups (G = 2,4,...,64, 64/G runs per wave): lane g holds row g in
+//                   registers and in LDS, the group evaluates every pairwise decision of the run
+//                   at once (each an exact sequential fp32 dot product; decisions are
+//                   symmetric), then replays the walk on the decision bits; after a merge only
+//                   the decisions of rows still to be visited against the new row are redone.
+//                   Longer runs are queued (big / huge / nestedCluster lists).
+//   k_merge_big     one workgroup per run of 65..kBigRows rows: the same scheme with the run's
+//                   rows and its decision matrix in LDS, kept in POSITION space so every step of
+//                   the walk is a few bit operations.
+//   k_merge_wave    runs longer than kBigRows: one wave per run, the reference order directly.
+//
+// Results are positional (survivors in place, kInvalid after), so they do not depend on which
+// wave handled which run or in what order.
+#include <algorithm>
+
+#include "klsh_device.cuh"
+
+namespace klsh {
+
+// ------------------------------------------------------------------------------- helpers -----
+__device__ __forceinline__ void lds_fence() {
+  // orders this workgroup's LDS stores before later LDS loads from other lanes of the same wave
+  // (LDS executes one wave's instructions in order) and stops the compiler moving memory ops
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
+  return (uint32_t)__shfl((int)v, (int)src, 64);
+}
+__device__ __forceinline__ float shflf(float v, uint32_t src) { return __shfl(v, (int)src, 64); }
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  const uint32_t lo = shfl32((uint32_t)v, src), hi = shfl32((uint32_t)(v >> 32), src);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint64_t lanes_below(uint32_t lane) {
+  return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+template <int D>
+__device__ __forceinline__ float dot_reg_lds(const float (&a)[D], const float* b) {
+  float s = 0.0f;
+#pragma unroll
+  for (int k = 0; k < D; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(b + k);
+    s = s + a[k] * v.x;
+    s = s + a[k + 1] * v.y;
+    s = s + a[k + 2] * v.z;
+    s = s + a[k + 3] * v.w;
+  }
+  return s;
+}
+
+template <int D>
+__device__ __forceinline__ float dot_lds_lds(const float* a, const float* b) {
+  float s = 0.0f;
+#pragma unroll
+  for (int k = 0; k < D; k += 4) {
+    const float4 u = *reinterpret_cast<const float4*>(a + k);
+    const float4 v = *reinterpret_cast<const float4*>(b + k);
+    s = s + u.x * v.x;
+    s = s + u.y * v.y;
+    s = s + u.z * v.z;
+    s = s + u.w * v.w;
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------- segments -----
+struct SrcHead {  // 1 at the first position of every run of equal keys in [lo, lo + n)
+  const uint32_t* key;
+  uint32_t lo;
+  __device__ uint32_t operator()(uint32_t i) const {
+    return (i == 0 || key[lo + i] != key[lo + i - 1]) ? 1u : 0u;
+  }
+};
+struct DstSegStart {
+  uint32_t* seg;
+  uint32_t lo;
+  __device__ void operator()(uint32_t i, uint32_t prefix, uint32_t v) const {
+    if (v) seg[prefix] = lo + i;
+  }
+};
+
+__device__ __forceinline__ int size_class(uint32_t b) {  // G = 2 << class lanes per run
+  return b <= 2 ? 0 : b <= 4 ? 1 : b <= 8 ? 2 : b <= 16 ? 3 : b <= 32 ? 4 : 5;
+}
+
+// Queue a long run (rare) to the big / huge / nestedCluster list.
+__device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucket_thr,
+                                               const MergeWork& w, Counters* ctr) {
+  if (bucket_thr >= 0 && b > (uint32_t)bucket_thr) {  // cluster.cc:286 -> nestedCluster
+    w.over[atomicAdd(&ctr->n_over, 1u)] = make_uint2(p, b);
+  } else if (b <= (uint32_t)kBigRows) {
+    w.big[atomicAdd(&ctr->n_big, 1u)] = make_uint2(p, b);
+  } else {
+    w.huge[atomicAdd(&ctr->n_huge, 1u)] = make_uint2(p, b);
+  }
+}
+
+// --------------------------------------------------------------------- G-lane groups -----
+// The wave handles n runs listed in LDS (ents), 64/G at a time.  Lane g of a group is position
+// g of its run and owns row id g: row in registers x[] and at LDS row `lane`.
+template <int G, int D>
+__device__ __forceinline__ void run_groups(const uint2* ents, uint32_t n, uint32_t* slots,
+                                           float thr, const Rows& r, float* lds) {
+  constexpr uint32_t NG = 64 / G;
+  constexpr int ST = D + 4;  // padded row stride: 16 lanes of a ds_read_b128 hit distinct banks
+  const uint32_t lane = threadIdx.x;
+  const uint32_t g = lane & (G - 1);
+  const uint32_t gbase = lane - g;
+  const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << G) - 1ull) << gbase);
+  float* myrow = lds + lane * ST;
+
+  for (uint32_t base = 0; base < n; base += NG) {
+    const uint32_t bi = base + lane / G;
+    uint32_t p = 0, b = 0;
+    if (bi < n) {
+      const uint2 e = ents[bi];
+      p = e.x;
+      b = e.y;
+    }
+    const bool valid = g < b;
+    const uint32_t slot = valid ? slots[p + g] : 0u;
+    float x[D];
+    if (valid) {
+      load_row<D>(r.x + (size_t)slot * r.dp, x);
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[k] = 0.0f;
+    }
+    float nrm = valid ? r.nrm[slot] : 0.0f;
+    uint32_t cnt = valid ? r.cnt[slot] : 0u;
+    uint32_t hd = valid ? r.head[slot] : 0u;
+    const uint32_t tl = valid ? r.tail[slot] : 0u;
+#pragma unroll
+    for (int k = 0; k < D; k += 4)
+      *reinterpret_cast<float4*>(myrow + k) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
+    lds_fence();
+    const uint32_t bmax = wave_max(b);
+
+    // 1. every pairwise decision of the run.  decide(a, c) == decide(c, a): the products, their
+    //    summation order and the sqrt product are the same either way.
+    uint64_t full = 0ull;
+    for (uint32_t j = 0; j + 1 < bmax; ++j) {
+      const float nj = shflf(nrm, gbase + j);
+      if (valid && g > j) {
+        const float dot = dot_reg_lds<D>(x, lds + (gbase + j) * ST);
+        if (cos_decide(dot, nrm, nj, thr)) full |= 1ull << j;
+      }
+    }
+    for (uint32_t c = 1; c < bmax; ++c) {
+      const uint64_t mc = shfl64(full, gbase + c);
+      if (c > g && ((mc >> g) & 1ull)) full |= 1ull << c;
+    }
+
+    // 2. replay the walk on the bits
+    uint32_t rowid = g;  // row id at my position
+    uint32_t mypos = g;  // position of my row
+    bool alive = valid, dirty = false;
+    uint32_t i = 1, size = b;  // uniform within the group
+    while (true) {
+      const bool active = i < size;
+      if (__ballot(active) == 0ull) break;
+      const uint32_t ic = active ? i : 0u;
+      const uint32_t rr = shfl32(rowid, gbase + ic);  // row being visited (the reference's i)
+      const uint64_t fr = shfl64(full, gbase + rr);
+      const bool hit = active && g < i && ((fr >> rowid) & 1ull);
+      const uint64_t m = __ballot(hit) & gmask;
+      if (m != 0ull) {
+        const uint32_t jpos = (uint32_t)(__ffsll((unsigned long long)m) - 1) - gbase;
+        const uint32_t c = shfl32(rowid, gbase + jpos);  // first matching candidate (row j)
+        const uint32_t ca = shfl32(cnt, gbase + rr), cb = shfl32(cnt, gbase + c);
+        const uint32_t hr = shfl32(hd, gbase + rr), tr = shfl32(tl, gbase + rr);
+        const uint32_t hc = shfl32(hd, gbase + c);
+        const uint32_t slot_c = shfl32(slot, gbase + c);
+        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+        const float* rowr = lds + (gbase + rr) * ST;
+        float* rowc = lds + (gbase + c) * ST;
+        float* xc = r.x + (size_t)slot_c * r.dp;
+        for (int k = (int)g; k < D; k += G) {  // consensus, split over the group's lanes
+          const float v = consensus(rowr[k], fa, rowc[k], fb, fn);
+          rowc[k] = v;
+          xc[k] = v;
+        }
+        lds_fence();
+        if (g == c) {  // new row c: registers, exact sequential norm, member list head
+          load_row<D>(rowc, x);
+          float nn = 0.0f;
+#pragma unroll
+          for (int k = 0; k < D; ++k) nn = nn + x[k] * x[k];
+          nrm = nn;
+          cnt = ca + cb;
+          hd = hr;
+          dirty = true;
+        }
+        if (g == rr) alive = false;
+        if (g == 0) r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
+        const uint32_t last = shfl32(rowid, gbase + size - 1);  // swap-remove
+        if (g == i) rowid = last;
+        if (g == last) mypos = i;
+        --size;
+        const float nc = shflf(nrm, gbase + c);
+        if (alive && mypos >= i && mypos < size) {  // rows still to be visited vs the new row c
+          const float dot = dot_reg_lds<D>(x, rowc);
+          full = cos_decide(dot, nrm, nc, thr) ? (full | (1ull << c)) : (full & ~(1ull << c));
+        }
+      } else if (active) {
+        ++i;
+      }
+    }
+
+    // 3. write back: survivors in position order, kInvalid after; changed rows' metadata
+    const uint32_t pos_slot = shfl32(slot, gbase + rowid);
+    if (valid) slots[p + g] = g < size ? pos_slot : kInvalid;
+    if (valid && alive && dirty) {
+      r.nrm[slot] = nrm;
+      r.cnt[slot] = cnt;
+      r.head[slot] = hd;
+    }
+    if (valid && !alive) r.cnt[slot] = 0u;
+    lds_fence();
+  }
+}
+
+// One wave per window of 64 runs (persistent over windows).
+template <int D>
+__global__ __launch_bounds__(64) void k_merge_window(const uint32_t* __restrict__ seg,
+                                                     uint32_t hi, int bucket_thr,
+                                                     uint32_t* __restrict__ slots, float thr,
+                                                     Rows r, MergeWork w, Counters* ctr) {
+  __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
+  __shared__ uint2 ents[64];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t lt = lanes_below(lane);
+  const uint32_t nseg = __hip_atomic_load(&ctr->n_seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nwin = (nseg + 63) / 64;
+  for (uint32_t win = blockIdx.x; win < nwin; win += gridDim.x) {
+    const uint32_t s = win * 64 + lane;
+    uint32_t p = 0, b = 0;
+    int cls = -1;
+    if (s < nseg) {
+      p = seg[s];
+      b = ((s + 1 < nseg) ? seg[s + 1] : hi) - p;
+      if ((bucket_thr >= 0 && b > (uint32_t)bucket_thr) || b > 64u) {
+        queue_long_run(p, b, bucket_thr, w, ctr);
+      } else if (b >= 2) {
+        cls = size_class(b);
+      }
+    }
+    uint32_t cnt[6];
+    uint32_t off = 0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {  // runs of this window grouped by class, position order kept
+      const uint64_t m = __ballot(cls == c);
+      if (cls == c) ents[off + (uint32_t)__popcll(m & lt)] = make_uint2(p, b);
+      cnt[c] = (uint32_t)__popcll(m);
+      off += cnt[c];
+    }
+    lds_fence();
+    off = 0;
+    if (cnt[0]) run_groups<2, D>(ents + off, cnt[0], slots, thr, r, lds);
+    off += cnt[0];
+    if (cnt[1]) run_groups<4, D>(ents + off, cnt[1], slots, thr, r, lds);
+    off += cnt[1];
+    if (cnt[2]) run_groups<8, D>(ents + off, cnt[2], slots, thr, r, lds);
+    off += cnt[2];
+    if (cnt[3]) run_groups<16, D>(ents + off, cnt[3], slots, thr, r, lds);
+    off += cnt[3];
+    if (cnt[4]) run_groups<32, D>(ents + off, cnt[4], slots, thr, r, lds);
+    off += cnt[4];
+    if (cnt[5]) run_groups<64, D>(ents + off, cnt[5], slots, thr, r, lds);
+    lds_fence();
+  }
+}
+
+// ----------------------------------------------------------------- runs of 65..kBigRows -----
+// One workgroup (4 waves) per run; the run's rows, norms, member bookkeeping and its decision
+// matrix live in LDS.  The matrix is kept in POSITION space: P[y] bit q = decide(row y, row at
+// position q), so the walk's "first j < i" is a find-first-set over <= kBigWords words.
+template <int D>
+struct BigLayout {
+  static constexpr int ST = D + 4;
+  static constexpr int W = kBigWords;
+  static constexpr size_t rows = 0;
+  static constexpr size_t P = rows + sizeof(float) * kBigRows * ST;
+  static constexpr size_t Q = P + sizeof(uint64_t) * kBigRows * W;
+  static constexpr size_t meta = Q + sizeof(uint64_t) * kBigRows * W;
+  static constexpr size_t bytes = meta + sizeof(uint32_t) * kBigRows * 6;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void k_merge_big(const uint2* __restrict__ list,
+                                                   uint32_t* __restrict__ slots, float thr, Rows r,
+                                                   Counters* ctr) {
+  using L = BigLayout<D>;
+  constexpr int ST = L::ST, W = L::W;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* rows = reinterpret_cast<float*>(smem + L::rows);
+  uint64_t* P = reinterpret_cast<uint64_t*>(smem + L::P);  // [row][W] position-space masks
+  uint64_t* Q = reinterpret_cast<uint64_t*>(smem + L::Q);  // [row][W] decisions vs later rows
+  uint32_t* slot = reinterpret_cast<uint32_t*>(smem + L::meta);
+  float* nrm = reinterpret_cast<float*>(slot + kBigRows);
+  uint32_t* cnt = slot + 2 * kBigRows;
+  uint32_t* hd = slot + 3 * kBigRows;
+  uint32_t* tl = slot + 4 * kBigRows;
+  uint32_t* pos2row = slot + 5 * kBigRows;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t count = __hip_atomic_load(&ctr->n_big, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    const uint2 e = list[li];
+    const uint32_t p = e.x, b = e.y;
+    // load the run
+    for (uint32_t a = t; a < b; a += 256) {
+      const uint32_t s = slots[p + a];
+      slot[a] = s;
+      nrm[a] = r.nrm[s];
+      cnt[a] = r.cnt[s];
+      hd[a] = r.head[s];
+      tl[a] = r.tail[s];
+      pos2row[a] = a;
+    }
+    for (uint32_t a = t; a < (uint32_t)kBigRows * W; a += 256) {
+      P[a] = 0ull;
+      Q[a] = 0ull;
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < b * (uint32_t)(D / 4); q += 256) {
+      const uint32_t a = q / (D / 4), k = (q % (D / 4)) * 4;
+      *reinterpret_cast<float4*>(rows + a * ST + k) =
+          *reinterpret_cast<const float4*>(r.x + (size_t)slot[a] * r.dp + k);
+    }
+    __syncthreads();
+    // decisions: thread a (row-stationary) against every earlier row c; at step c the wave's
+    // lanes all read row c (LDS broadcast) and the wave's ballot is P[c]'s word for its rows.
+    for (uint32_t a0 = wv * 64; a0 < b; a0 += 256) {
+      const uint32_t a = a0 + lane;
+      float xa[D];
+      if (a < b) {
+        load_row<D>(rows + a * ST, xa);
+      } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) xa[k] = 0.0f;
+      }
+      const float na = a < b ? nrm[a] : 0.0f;
+      uint64_t own[W];
+#pragma unroll
+      for (int k = 0; k < W; ++k) own[k] = 0ull;
+      const uint32_t cend = min(b, a0 + 64u) - 1;  // last row any lane of this wave needs
+      for (uint32_t c = 0; c < cend; ++c) {
+        bool dc = false;
+        if (a < b && c < a) dc = cos_decide(dot_reg_lds<D>(xa, rows + c * ST), na, nrm[c], thr);
+        const uint64_t m = __ballot(dc);  // rows a0..a0+63 that match row c
+        if (lane == 0) Q[c * W + a0 / 64] = m;
+#pragma unroll
+        for (int k = 0; k < W; ++k)
+          if ((uint32_t)k == c / 64 && dc) own[k] |= 1ull << (c & 63u);
+      }
+      if (a < b) {
+#pragma unroll
+        for (int k = 0; k < W; ++k) P[a * W + k] = own[k];
+      }
+    }
+    __syncthreads();
+    for (uint32_t a = t; a < b * (uint32_t)W; a += 256) P[a] |= Q[a];  // symmetric
+    __syncthreads();
+
+    // the walk, by wave 0
+    if (wv == 0) {
+      uint32_t i = 1, size = b;
+      while (i < size) {
+        const uint32_t rr = pos2row[i];
+        // first position j < i with P[rr] bit j
+        uint64_t word = 0ull;
+        if (lane < (uint32_t)W) {
+          word = P[rr * W + lane];
+          const uint32_t lo = lane * 64u;
+          if (lo >= i) word = 0ull;
+          else if (i - lo < 64u) word &= (1ull << (i - lo)) - 1ull;
+        }
+        const uint64_t nz = __ballot(word != 0ull);
+        if (nz == 0ull) {
+          ++i;
+          continue;
+        }
+        const uint32_t wd = (uint32_t)(__ffsll((unsigned long long)nz) - 1);
+        const uint64_t wbits = shfl64(word, wd);
+        const uint32_t j = wd * 64u + (uint32_t)(__ffsll((unsigned long long)wbits) - 1);
+        const uint32_t c = pos2row[j];
+        const uint32_t ca = cnt[rr], cb = cnt[c];
+        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+        float* rowc = rows + c * ST;
+        const float* rowr = rows + rr * ST;
+        float* xc = r.x + (size_t)slot[c] * r.dp;
+        for (int k = (int)lane; k < D; k += 64) {
+          const float v = consensus(rowr[k], fa, rowc[k], fb, fn);
+          rowc[k] = v;
+          xc[k] = v;
+        }
+        lds_fence();
+        if (lane == 0) {
+          float nn = 0.0f;
+          for (int k = 0; k < D; ++k) nn = nn + rowc[k] * rowc[k];
+          nrm[c] = nn;
+          r.nxt[tl[rr]] = hd[c];  // ids_current ++ ids_candidate
+          hd[c] = hd[rr];
+          cnt[c] = ca + cb;
+          cnt[rr] = 0u;
+          pos2row[i] = pos2row[size - 1];  // swap-remove
+        }
+        lds_fence();
+        --size;
+        const float nc = nrm[c];
+        const uint32_t moved = size;  // old position of the row now at i
+        for (uint32_t q = i + lane; q < size; q += 64) {  // rows still to be visited
+          const uint32_t y = pos2row[q];
+          uint64_t* Py = P + y * W;
+          // the row that sat at position `moved` is now at position i
+          const bool bm = (Py[moved / 64] >> (moved & 63u)) & 1ull;
+          Py[moved / 64] &= ~(1ull << (moved & 63u));
+          Py[i / 64] = bm ? (Py[i / 64] | (1ull << (i & 63u))) : (Py[i / 64] & ~(1ull << (i & 63u)));
+          const bool dn = cos_decide(dot_lds_lds<D>(rows + y * ST, rowc), nrm[y], nc, thr);
+          Py[j / 64] = dn ? (Py[j / 64] | (1ull << (j & 63u))) : (Py[j / 64] & ~(1ull << (j & 63u)));
+        }
+        lds_fence();
+      }
+      // write back
+      for (uint32_t q = lane; q < b; q += 64) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
+      for (uint32_t q = lane; q < size; q += 64) {
+        const uint32_t y = pos2row[q];
+        r.nrm[slot[y]] = nrm[y];
+        r.cnt[slot[y]] = cnt[y];
+        r.head[slot[y]] = hd[y];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- runs longer than that -----
+// One wave per run, the reference order directly: for the visited row i the lanes test
+// candidates j = c*64 + lane, the lowest lane of the first chunk with a hit is the first match.
+template <int D>
+__global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ list,
+                                                   const uint32_t* count_ptr,
+                                                   uint32_t* __restrict__ slots, float thr, Rows r) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];  // consensus row for the norm
+  const uint32_t lane = threadIdx.x;
+  const uint32_t count = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int d = r.d;
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    const uint2 e = list[li];
+    const uint32_t p = e.x, b = e.y;
+    uint32_t* s = slots + p;
+    uint32_t size = b, i = 1;
+    while (i < size) {
+      const uint32_t si = s[i];
+      const float* xip = r.x + (size_t)si * r.dp;
+      const float ni = r.nrm[si];
+      int found = -1;
+      if constexpr (D > 0) {
+        float xi[D > 0 ? D : 4];
+        load_row<(D > 0 ? D : 4)>(xip, xi);
+        for (uint32_t c = 0; c < i; c += 64) {
+          const uint32_t j = c + lane;
+          bool ok = false;
+          if (j < i) {
+            const uint32_t sj = s[j];
+            ok = cos_decide(dot_reg_mem<(D > 0 ? D : 4)>(xi, r.x + (size_t)sj * r.dp), ni,
+                            r.nrm[sj], thr);
+          }
+          const uint64_t m = __ballot(ok);
+          if (m) {
+            found = (int)(c + (uint32_t)(__ffsll((unsigned long long)m) - 1));
+            break;
+          }
+        }
+      } else {
+        for (uint32_t c = 0; c < i; c += 64) {
+          const uint32_t j = c + lane;
+          bool ok = false;
+          if (j < i) {
+            const uint32_t sj = s[j];
+            ok = cos_decide(dot_mem_mem(xip, r.x + (size_t)sj * r.dp, d), ni, r.nrm[sj], thr);
+          }
+          const uint64_t m = __ballot(ok);
+          if (m) {
+            found = (int)(c + (uint32_t)(__ffsll((unsigned long long)m) - 1));
+            break;
+          }
+        }
+      }
+      if (found >= 0) {
+        const uint32_t sj = s[found];
+        float* xj = r.x + (size_t)sj * r.dp;
+        const uint32_t ca = r.cnt[si], cb = r.cnt[sj];
+        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+        for (int kk = lane; kk < d; kk += 64) {
+          const float v = consensus(xip[kk], fa, xj[kk], fb, fn);
+          sx[kk] = v;
+          xj[kk] = v;
+        }
+        __syncthreads();
+        if (lane == 0) {
+          float nn = 0.0f;
+          for (int kk = 0; kk < d; ++kk) nn = nn + sx[kk] * sx[kk];
+          r.nrm[sj] = nn;
+          link_members(r, si, sj);
+          s[i] = s[size - 1];
+        }
+        __syncthreads();
+        --size;
+      } else {
+        ++i;
+      }
+    }
+    for (uint32_t t = size + lane; t < b; t += 64) s[t] = kInvalid;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------- widths without a -----
+// register kernel: one lane per run of 2..64 rows, the reference order directly, rows from
+// memory; longer runs go to the wave kernel.
+__global__ __launch_bounds__(256) void k_merge_lane_generic(const uint32_t* __restrict__ seg,
+                                                            uint32_t hi, int bucket_thr,
+                                                            uint32_t* __restrict__ slots,
+                                                            float thr, Rows r, MergeWork w,
+                                                            Counters* ctr) {
+  const uint32_t nseg = __hip_atomic_load(&ctr->n_seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int d = r.d;
+  for (uint32_t sidx = blockIdx.x * 256u + threadIdx.x; sidx < nseg; sidx += gridDim.x * 256u) {
+    const uint32_t p = seg[sidx];
+    const uint32_t b = ((sidx + 1 < nseg) ? seg[sidx + 1] : hi) - p;
+    if ((bucket_thr >= 0 && b > (uint32_t)bucket_thr) || b > 64u) {
+      if (bucket_thr >= 0 && b > (uint32_t)bucket_thr)
+        w.over[atomicAdd(&ctr->n_over, 1u)] = make_uint2(p, b);
+      else
+        w.huge[atomicAdd(&ctr->n_huge, 1u)] = make_uint2(p, b);
+      continue;
+    }
+    uint32_t* s = slots + p;
+    uint32_t size = b, i = 1;
+    while (i < size) {
+      const uint32_t si = s[i];
+      const float* xi = r.x + (size_t)si * r.dp;
+      const float ni = r.nrm[si];
+      uint32_t j = 0;
+      for (; j < i; ++j) {
+        const uint32_t sj = s[j];
+        if (cos_decide(dot_mem_mem(xi, r.x + (size_t)sj * r.dp, d), ni, r.nrm[sj], thr)) break;
+      }
+      if (j < i) {
+        const uint32_t sj = s[j];
+        float* xj = r.x + (size_t)sj * r.dp;
+        const float fa = (float)(int)r.cnt[si], fb = (float)(int)r.cnt[sj];
+        const float fn = (float)(int)(r.cnt[si] + r.cnt[sj]);
+        float nn = 0.0f;
+        for (int k = 0; k < d; ++k) {
+          const float v = consensus(xi[k], fa, xj[k], fb, fn);
+          xj[k] = v;
+          nn = nn + v * v;
+        }
+        r.nrm[sj] = nn;
+        link_members(r, si, sj);
+        s[i] = s[size - 1];
+        --size;
+      } else {
+        ++i;
+      }
+    }
+    for (uint32_t t = size; t < b; ++t) s[t] = kInvalid;
+  }
+}
+
+// ----------------------------------------------------------------------------- launch -----
+template <int D>
+static void launch_window(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
+                          uint32_t* slots, float thr, const MergeWork& w, Counters* ctr,
+                          uint32_t n, hipStream_t s) {
+  // Persistent grids: run counts live on the device; each grid strides over its work.
+  const uint32_t g1 = (uint32_t)std::min<uint64_t>(8192, (n + 63) / 64 + 1);
+  k_merge_window<D><<<g1, 64, 0, s>>>(seg, hi, bucket_thr, slots, thr, r, w, ctr);
+  static bool lds_ok = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_big<D>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)BigLayout<D>::bytes) == hipSuccess;
+  }();
+  (void)lds_ok;
+  const uint32_t g2 = (uint32_t)std::min<uint64_t>(1024, n / 65 + 1);
+  k_merge_big<D><<<g2, 256, BigLayout<D>::bytes, s>>>(w.big, slots, thr, r, ctr);
+  const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows + 1) + 1);
+  k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, thr, r);
+}
+
+void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
+                  float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s) {
+  if (hi <= lo) return;
+  const uint32_t n = hi - lo;
+  device_scan(SrcHead{key, lo}, DstSegStart{w.seg, lo}, n, w.tile_sums, &ctr->n_seg, s);
+  switch (r.d) {
+    case 8: launch_window<8>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    case 16: launch_window<16>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    case 32: launch_window<32>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    case 64: launch_window<64>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    default: {
+      const uint32_t g1 = (uint32_t)std::min<uint64_t>(4096, (n + 255) / 256);
+      k_merge_lane_generic<<<g1, 256, 0, s>>>(w.seg, hi, bucket_thr, slots, thr, r, w, ctr);
+      const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / 65 + 1);
+      k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, thr, r);
+    }
+  }
+}
+
+}  // namespace klsh

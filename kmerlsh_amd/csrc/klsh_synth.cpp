@@ -18,7 +18,19 @@
 #include <thread>
 #include <vector>
 
+#include <cstdlib>
+
 namespace {
+
+// Host worker threads: OMP_NUM_THREADS if set (the GPU boxes set it to their CPU share), else
+// min(16, hardware threads).
+static int klsh_default_threads() {
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int v = std::atoi(e);
+    if (v > 0) return v;
+  }
+  return (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+}
 
 inline uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -35,7 +47,7 @@ inline double gauss(uint64_t a, uint64_t b) {
 
 template <class F>
 void parallel_for(uint64_t n, int threads, F f) {
-  if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (threads <= 0) threads = klsh_default_threads();
   threads = (int)std::min<uint64_t>((uint64_t)threads, std::max<uint64_t>(1, n));
   std::vector<std::thread> pool;
   const uint64_t chunk = (n + threads - 1) / threads;

@@ -74,6 +74,19 @@ def test_pcluster_matches_reference(engine, name):
     assert_same_result(engine.result(), z["out_rows"], z["out_off"], z["out_ids"])
 
 
+@pytest.mark.parametrize("b,d,groups,noise,thr", [
+    (65, 64, 6, 0.05, 0.9), (200, 32, 12, 0.08, 0.85), (384, 64, 30, 0.05, 0.95),
+    (385, 64, 30, 0.05, 0.95), (700, 16, 50, 0.1, 0.8), (64, 8, 3, 0.2, 0.9), (3, 64, 1, 0.01, 0.9),
+])
+def test_pcluster_run_lengths_vs_oracle(engine, oracle, b, d, groups, noise, thr):
+    """Every merge path by bucket length: G-lane groups (<= 64), LDS matrix (65..384), wave (> 384)."""
+    rng = np.random.default_rng(b * 7 + d)
+    rows = clustered(rng, b, d, groups, noise)
+    engine.load_rows(rows)
+    engine.pcluster(thr)
+    assert_same_result(engine.result(), *oracle.pcluster(rows, thr))
+
+
 @pytest.mark.parametrize("b,d", [(33, 64), (1000, 16), (5000, 8)])
 def test_pcluster_identical_rows(engine, oracle, b, d):
     """Degenerate bucket (every row identical): the wave kernel merges i into j = 0 each step."""

@@ -14,14 +14,14 @@ import pytest
 from conftest import ROOT
 
 CSRC = os.path.join(ROOT, "kmerlsh_amd", "csrc")
-ASM = os.path.join(ROOT, "kmerlsh_amd", "build", "klsh_kernels.s")
+ASMS = [os.path.join(ROOT, "kmerlsh_amd", "build", f) for f in ("klsh_kernels.s", "klsh_merge.s")]
 FMA = re.compile(r"^\s+(v_fma\w*|v_fmac\w*|v_pk_fma\w*|v_mad_f32\w*|v_fmamk\w*|v_fmaak\w*)\b")
 
 
 @pytest.fixture(scope="module")
 def kernels():
     subprocess.run(["make", "-s", "-C", CSRC, "isa"], check=True)
-    text = open(ASM).read()
+    text = "".join(open(a).read() for a in ASMS)
     out = {}
     for m in re.finditer(r"^(_Z\w+):[^\n]*\n(.*?)^\.Lfunc_end", text, re.M | re.S):
         out[m.group(1)] = m.group(2)
@@ -30,8 +30,8 @@ def kernels():
 
 
 def test_target_is_gfx950(kernels):
-    text = open(ASM).read()
-    assert "gfx950" in text
+    for a in ASMS:
+        assert "gfx950" in open(a).read()
 
 
 def test_projection_has_no_fused_multiply_add(kernels):
