@@ -130,6 +130,7 @@ struct klsh_ctx {
     dfree(rows.nxt); dfree(order); dfree(alt); dfree(keys); dfree(keys2); dfree(nk1);
     dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.seg); dfree(mw.over);
     dfree(mw.big); dfree(mw.huge);
+    for (auto& c : mw.cls) dfree(c);
     cap_slots = cap_members = 0;
     cap_dp = 0;
     drop_snapshot();
@@ -178,6 +179,12 @@ struct klsh_ctx {
         (e = dalloc(&mw.big, s / 65 + 64)) || (e = dalloc(&mw.huge, s / (klsh::kBigRows + 1) + 64))) {
       release_state();
       return e;
+    }
+    for (int c = 0; c < klsh::kGroupClasses; ++c) {
+      if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s)))) {
+        release_state();
+        return e;
+      }
     }
     mw.tile_sums = tile_sums;
     cap_slots = s;

@@ -18,22 +18,29 @@ constexpr int kScanTile = 4096;             // items per scan workgroup (256 lan
 constexpr int kBigRows = 384;
 constexpr int kBigWords = kBigRows / 64;
 
+// Runs of 2..64 rows are merged by G-lane groups, one size class per G = 2, 4, ..., 64
+// (class c holds runs of 2^c < b <= 2^(c+1) rows).
+constexpr int kGroupClasses = 6;
+inline uint64_t group_class_capacity(int c, uint64_t cap) { return cap / ((1ull << c) + 1) + 64; }
+
 // Device-side per-iteration counters (zeroed by the host before each iteration).
 struct Counters {
-  uint32_t n_seg;   // bucket runs found by the segment scan
-  uint32_t n_big;   // runs of 65..kBigRows rows queued for k_merge_big
-  uint32_t n_huge;  // runs longer than kBigRows queued for k_merge_wave
-  uint32_t n_over;  // runs longer than bucket_size_threshold (nestedCluster)
-  uint32_t total;   // result of the last scan/compaction (live rows)
-  uint32_t pad[11];
+  uint32_t n_seg;                  // bucket runs found by the segment scan
+  uint32_t n_cls[kGroupClasses];   // runs of 2..64 rows queued per size class
+  uint32_t n_big;                  // runs of 65..kBigRows rows queued for k_merge_big
+  uint32_t n_huge;                 // runs longer than kBigRows queued for k_merge_wave
+  uint32_t n_over;                 // runs longer than bucket_size_threshold (nestedCluster)
+  uint32_t total;                  // result of the last scan/compaction (live rows)
+  uint32_t pad[5];
 };
 
 // Merge workspace (device), sized for `cap` positions.
 struct MergeWork {
-  uint32_t* seg;   // run starts [n_seg]
-  uint2* big;      // (start, length) of runs for k_merge_big
-  uint2* huge;     // (start, length) of runs for k_merge_wave
-  uint2* over;     // (start, length) of oversize runs
+  uint32_t* seg;                   // run starts [n_seg]
+  uint2* cls[kGroupClasses];       // (start, length) of runs per size class
+  uint2* big;                      // (start, length) of runs for k_merge_big
+  uint2* huge;                     // (start, length) of runs for k_merge_wave
+  uint2* over;                     // (start, length) of oversize runs
   uint32_t* tile_sums;
 };
 

@@ -8,13 +8,14 @@
 // of a merge changes, so the GPU version evaluates decisions in bulk and replays the walk:
 //
 //   segment scan    bucket runs = positions where the sorted key changes (parallel scan)
-//   k_merge_window  one wave per window of 64 runs.  Runs of 2..64 rows are handled in place by
-//                   G-lane groups (G = 2,4,...,64, 64/G runs per wave): lane g holds row g in
+//   k_classify      runs of 2..64 rows to size-class lists; longer runs to big / huge /
+//                   nestedCluster lists
+//   k_merge_group   runs of 2..64 rows, in place, by G-lane groups (G = 2,4,...,64; 64/G runs
+//                   per wave, one kernel per class): lane g holds row g in
 //                   registers and in LDS, the group evaluates every pairwise decision of the run
 //                   at once (each an exact sequential fp32 dot product; decisions are
 //                   symmetric), then replays the walk on the decision bits; after a merge only
 //                   the decisions of rows still to be visited against the new row are redone.
-//                   Longer runs are queued (big / huge / nestedCluster lists).
 //   k_merge_big     one workgroup per run of 65..kBigRows rows: the same scheme with the run's
 //                   rows and its decision matrix in LDS, kept in POSITION space so every step of
 //                   the walk is a few bit operations.
@@ -238,55 +239,58 @@ __device__ __forceinline__ void run_groups(const uint2* ents, uint32_t n, uint32
   }
 }
 
-// One wave per window of 64 runs (persistent over windows).
-template <int D>
-__global__ __launch_bounds__(64) void k_merge_window(const uint32_t* __restrict__ seg,
-                                                     uint32_t hi, int bucket_thr,
-                                                     uint32_t* __restrict__ slots, float thr,
-                                                     Rows r, MergeWork w, Counters* ctr) {
-  __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
-  __shared__ uint2 ents[64];
-  const uint32_t lane = threadIdx.x;
-  const uint64_t lt = lanes_below(lane);
+// One lane per run: runs of 2..64 rows go to their size-class list, longer ones to the big /
+// huge / nestedCluster lists.  Offsets are aggregated per wave (ballot) and per workgroup (LDS),
+// so each workgroup issues one global atomic per class.
+__global__ __launch_bounds__(1024) void k_classify(const uint32_t* __restrict__ seg, uint32_t hi,
+                                                   int bucket_thr, MergeWork w, Counters* ctr) {
+  __shared__ uint32_t bcnt[kGroupClasses], bbase[kGroupClasses];
   const uint32_t nseg = __hip_atomic_load(&ctr->n_seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nwin = (nseg + 63) / 64;
-  for (uint32_t win = blockIdx.x; win < nwin; win += gridDim.x) {
-    const uint32_t s = win * 64 + lane;
-    uint32_t p = 0, b = 0;
-    int cls = -1;
-    if (s < nseg) {
-      p = seg[s];
-      b = ((s + 1 < nseg) ? seg[s + 1] : hi) - p;
-      if ((bucket_thr >= 0 && b > (uint32_t)bucket_thr) || b > 64u) {
-        queue_long_run(p, b, bucket_thr, w, ctr);
-      } else if (b >= 2) {
-        cls = size_class(b);
-      }
+  if (blockIdx.x * 1024u >= nseg) return;  // whole workgroup past the end
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  const uint64_t lt = lanes_below(lane);
+  if (t < (uint32_t)kGroupClasses) bcnt[t] = 0u;
+  __syncthreads();
+  const uint32_t s = blockIdx.x * 1024u + t;
+  uint32_t p = 0, b = 0;
+  int cls = -1;
+  if (s < nseg) {
+    p = seg[s];
+    b = ((s + 1 < nseg) ? seg[s + 1] : hi) - p;
+    if ((bucket_thr >= 0 && b > (uint32_t)bucket_thr) || b > 64u) {
+      queue_long_run(p, b, bucket_thr, w, ctr);
+    } else if (b >= 2) {
+      cls = size_class(b);
     }
-    uint32_t cnt[6];
-    uint32_t off = 0;
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {  // runs of this window grouped by class, position order kept
-      const uint64_t m = __ballot(cls == c);
-      if (cls == c) ents[off + (uint32_t)__popcll(m & lt)] = make_uint2(p, b);
-      cnt[c] = (uint32_t)__popcll(m);
-      off += cnt[c];
-    }
-    lds_fence();
-    off = 0;
-    if (cnt[0]) run_groups<2, D>(ents + off, cnt[0], slots, thr, r, lds);
-    off += cnt[0];
-    if (cnt[1]) run_groups<4, D>(ents + off, cnt[1], slots, thr, r, lds);
-    off += cnt[1];
-    if (cnt[2]) run_groups<8, D>(ents + off, cnt[2], slots, thr, r, lds);
-    off += cnt[2];
-    if (cnt[3]) run_groups<16, D>(ents + off, cnt[3], slots, thr, r, lds);
-    off += cnt[3];
-    if (cnt[4]) run_groups<32, D>(ents + off, cnt[4], slots, thr, r, lds);
-    off += cnt[4];
-    if (cnt[5]) run_groups<64, D>(ents + off, cnt[5], slots, thr, r, lds);
-    lds_fence();
   }
+  uint32_t myoff = 0;
+#pragma unroll
+  for (int c = 0; c < kGroupClasses; ++c) {
+    const uint64_t m = __ballot(cls == c);
+    if (m == 0ull) continue;
+    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+    uint32_t woff = 0;
+    if (lane == leader) woff = atomicAdd(&bcnt[c], (uint32_t)__popcll(m));
+    woff = shfl32(woff, leader);
+    if (cls == c) myoff = woff + (uint32_t)__popcll(m & lt);
+  }
+  __syncthreads();
+  if (t < (uint32_t)kGroupClasses && bcnt[t]) bbase[t] = atomicAdd(&ctr->n_cls[t], bcnt[t]);
+  __syncthreads();
+  if (cls >= 0) w.cls[cls][bbase[cls] + myoff] = make_uint2(p, b);
+}
+
+// One wave per batch of 64/G runs of one size class (persistent over the class list).
+template <int G, int D>
+__global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ list, int cls,
+                                                    uint32_t* __restrict__ slots, float thr,
+                                                    Rows r, Counters* ctr) {
+  __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
+  constexpr uint32_t NG = 64 / G;
+  const uint32_t n = __hip_atomic_load(&ctr->n_cls[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nb = (n + NG - 1) / NG;
+  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x)
+    run_groups<G, D>(list + bi * NG, min(NG, n - bi * NG), slots, thr, r, lds);
 }
 
 // ----------------------------------------------------------------- runs of 65..kBigRows -----
@@ -591,12 +595,20 @@ __global__ __launch_bounds__(256) void k_merge_lane_generic(const uint32_t* __re
 
 // ----------------------------------------------------------------------------- launch -----
 template <int D>
-static void launch_window(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
+static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
                           uint32_t* slots, float thr, const MergeWork& w, Counters* ctr,
                           uint32_t n, hipStream_t s) {
-  // Persistent grids: run counts live on the device; each grid strides over its work.
-  const uint32_t g1 = (uint32_t)std::min<uint64_t>(8192, (n + 63) / 64 + 1);
-  k_merge_window<D><<<g1, 64, 0, s>>>(seg, hi, bucket_thr, slots, thr, r, w, ctr);
+  k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
+  // Persistent grids: run counts live on the device; each grid strides over its list.
+  auto grid = [&](int c, uint32_t per_wave) {
+    return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
+  };
+  k_merge_group<2, D><<<grid(0, 32), 64, 0, s>>>(w.cls[0], 0, slots, thr, r, ctr);
+  k_merge_group<4, D><<<grid(1, 16), 64, 0, s>>>(w.cls[1], 1, slots, thr, r, ctr);
+  k_merge_group<8, D><<<grid(2, 8), 64, 0, s>>>(w.cls[2], 2, slots, thr, r, ctr);
+  k_merge_group<16, D><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, thr, r, ctr);
+  k_merge_group<32, D><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, thr, r, ctr);
+  k_merge_group<64, D><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, thr, r, ctr);
   static bool lds_ok = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_big<D>),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -615,10 +627,10 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   const uint32_t n = hi - lo;
   device_scan(SrcHead{key, lo}, DstSegStart{w.seg, lo}, n, w.tile_sums, &ctr->n_seg, s);
   switch (r.d) {
-    case 8: launch_window<8>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
-    case 16: launch_window<16>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
-    case 32: launch_window<32>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
-    case 64: launch_window<64>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    case 8: launch_groups<8>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    case 16: launch_groups<16>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    case 32: launch_groups<32>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    case 64: launch_groups<64>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
     default: {
       const uint32_t g1 = (uint32_t)std::min<uint64_t>(4096, (n + 255) / 256);
       k_merge_lane_generic<<<g1, 256, 0, s>>>(w.seg, hi, bucket_thr, slots, thr, r, w, ctr);
