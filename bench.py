@@ -163,12 +163,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "none"])
+    ap.add_argument("--iterations", type=int, default=0,
+                    help="profiling only: override the config's -I (the metric is then not C2's)")
     args = ap.parse_args()
 
     world, rank, local = dist_setup()
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
     n0, d, iters, min_sim, desc = CONFIGS[args.config]
+    if args.iterations:
+        iters = args.iterations
+        desc += f" [profiling override: -I {iters}]"
     from kmerlsh_amd import _native
 
     eng = _native.Engine(local)

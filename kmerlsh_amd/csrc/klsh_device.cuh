@@ -52,6 +52,32 @@ __device__ __forceinline__ float dot_reg_mem(const float (&a)[D], const float* _
   return s;
 }
 
+// Coalesced gather of the 64 rows owned by the lanes of a wave (lane l's row is slot `slot`,
+// present if `valid`) into an LDS tile with padded row stride D + 4 floats.  Each wave
+// instruction moves 64/(D/4) whole rows (D/4 lanes per row, 16 B per lane) instead of 64
+// scattered 16-B pieces; afterwards lane l reads its row from tile + l * (D + 4) (the padding
+// keeps those row-per-lane reads free of bank conflicts).
+template <int D>
+__device__ __forceinline__ void stage_rows(const float* __restrict__ X, int dp, uint32_t slot,
+                                           bool valid, float* tile) {
+  constexpr int CPR = D / 4;     // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;  // rows per wave instruction
+  const uint32_t lane = __lane_id();
+  const uint32_t q = lane % CPR, rsub = lane / CPR;
+  float4 v[CPR];
+#pragma unroll
+  for (int it = 0; it < CPR; ++it) {
+    const uint32_t row = it * RPI + rsub;
+    const uint32_t s = (uint32_t)__shfl((int)slot, (int)row, 64);
+    const int ok = __shfl(valid ? 1 : 0, (int)row, 64);
+    v[it] = ok ? *reinterpret_cast<const float4*>(X + (size_t)s * dp + 4 * q)
+               : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+#pragma unroll
+  for (int it = 0; it < CPR; ++it)
+    *reinterpret_cast<float4*>(tile + (it * RPI + rsub) * (D + 4) + 4 * q) = v[it];
+}
+
 __device__ __forceinline__ float dot_mem_mem(const float* a, const float* b, int d) {
   float s = 0.0f;
   for (int k = 0; k < d; ++k) s = s + a[k] * b[k];

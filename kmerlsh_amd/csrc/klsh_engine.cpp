@@ -533,6 +533,9 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   const float sim_step = (max_similarity - min_similarity) / (float)iterations;
   float threshold = max_similarity;
 
+  // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
+  // lshash.cc:36-42), so repeated timed calls never reuse a previous call's tables.
+  ctx->w_count = 0;
   // Pre-draw the hyperplanes this call can need without nested buckets (h_t is non-increasing).
   if (ctx->n_live > 0 && iterations > 0) {
     const uint64_t hmax = (uint64_t)floor_log2(ctx->n_live);

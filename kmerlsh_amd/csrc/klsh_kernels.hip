@@ -15,28 +15,56 @@
 //   k_scan_*        survivor compaction        (reference cluster.cc:39-45 merge_abundance)
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include "klsh_device.cuh"
 
 namespace klsh {
 
 // ========================================================================= projection ==========
 // One lane per live row; the row sits in registers, the h hyperplanes in LDS (broadcast reads).
-// Loop order per hyperplane is the reference's: s = ((0 + w0 x0) + w1 x1) + ...
-template <int D>
+// STAGED: rows are gathered coalesced through a per-wave LDS tile (stage_rows); otherwise each
+// lane loads its own row.  Four hyperplanes are summed at once (four independent chains); the
+// order inside each is the reference's: s = ((0 + w0 x0) + w1 x1) + ...
+template <int D, bool STAGED>
 __global__ __launch_bounds__(256) void k_project(const float* __restrict__ X, int dp,
                                                  const uint32_t* __restrict__ slots,
                                                  uint32_t* __restrict__ keys, uint32_t n,
                                                  const float* __restrict__ W, int h,
                                                  uint32_t key_or) {
   __shared__ __attribute__((aligned(16))) float sw[kMaxHyperplanes * D];
+  __shared__ __attribute__((aligned(16))) float tile[STAGED ? 4 : 1][STAGED ? 64 * (D + 4) : 4];
   for (int i = threadIdx.x; i < h * D; i += 256) sw[i] = W[(i / D) * dp + (i % D)];
-  __syncthreads();
   const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-  if (p >= n) return;
+  const bool valid = p < n;
   float x[D];
-  load_row<D>(X + (size_t)slots[p] * dp, x);
+  if constexpr (STAGED) {
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    stage_rows<D>(X, dp, valid ? slots[p] : 0u, valid, tile[wv]);
+    __syncthreads();
+    if (!valid) return;
+    load_row<D>(tile[wv] + lane * (D + 4), x);
+  } else {
+    __syncthreads();
+    if (!valid) return;
+    load_row<D>(X + (size_t)slots[p] * dp, x);
+  }
   uint32_t key = 0;
-  for (int j = 0; j < h; ++j) {
+  int j = 0;
+  for (; j + 4 <= h; j += 4) {
+    const float* w0 = sw + j * D;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      s0 = s0 + w0[k] * x[k];
+      s1 = s1 + w0[D + k] * x[k];
+      s2 = s2 + w0[2 * D + k] * x[k];
+      s3 = s3 + w0[3 * D + k] * x[k];
+    }
+    key = key * 16u + (s0 >= 0.0f ? 8u : 0u) + (s1 >= 0.0f ? 4u : 0u) + (s2 >= 0.0f ? 2u : 0u) +
+          (s3 >= 0.0f ? 1u : 0u);
+  }
+  for (; j < h; ++j) {
     const float* w = sw + j * D;
     float s = 0.0f;
 #pragma unroll
@@ -90,11 +118,23 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
                     const float* W, int h, uint32_t key_or, hipStream_t s) {
   if (n == 0) return;
   const dim3 grid((n + 255) / 256), block(256);
+  static const bool staged = [] {
+    const char* e = getenv("KLSH_PROJECT_STAGED");
+    return e && e[0] == '1';
+  }();
   switch (r.d) {
-    case 8: k_project<8><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
-    case 16: k_project<16><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
-    case 32: k_project<32><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
-    case 64: k_project<64><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
+#define KLSH_PROJECT_CASE(DD)                                                                    \
+  case DD:                                                                                     \
+    if (staged)                                                                                \
+      k_project<DD, true><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
+    else                                                                                       \
+      k_project<DD, false><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);    \
+    break;
+    KLSH_PROJECT_CASE(8)
+    KLSH_PROJECT_CASE(16)
+    KLSH_PROJECT_CASE(32)
+    KLSH_PROJECT_CASE(64)
+#undef KLSH_PROJECT_CASE
     default:
       k_project_generic<<<grid, block, 0, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or);
   }

@@ -68,6 +68,26 @@ __device__ __forceinline__ float dot_reg_lds(const float (&a)[D], const float* b
 }
 
 template <int D>
+__device__ __forceinline__ void dot2_reg_lds(const float (&a)[D], const float* b0, const float* b1,
+                                             float& s0, float& s1) {
+  s0 = 0.0f;
+  s1 = 0.0f;
+#pragma unroll
+  for (int k = 0; k < D; k += 4) {
+    const float4 u = *reinterpret_cast<const float4*>(b0 + k);
+    const float4 v = *reinterpret_cast<const float4*>(b1 + k);
+    s0 = s0 + a[k] * u.x;
+    s1 = s1 + a[k] * v.x;
+    s0 = s0 + a[k + 1] * u.y;
+    s1 = s1 + a[k + 1] * v.y;
+    s0 = s0 + a[k + 2] * u.z;
+    s1 = s1 + a[k + 2] * v.z;
+    s0 = s0 + a[k + 3] * u.w;
+    s1 = s1 + a[k + 3] * v.w;
+  }
+}
+
+template <int D>
 __device__ __forceinline__ float dot_lds_lds(const float* a, const float* b) {
   float s = 0.0f;
 #pragma unroll
@@ -125,7 +145,7 @@ __device__ __forceinline__ void run_groups(const uint2* ents, uint32_t n, uint32
   const uint32_t lane = threadIdx.x;
   const uint32_t g = lane & (G - 1);
   const uint32_t gbase = lane - g;
-  const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << G) - 1ull) << gbase);
+  const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << (G & 63)) - 1ull) << gbase);
   float* myrow = lds + lane * ST;
 
   for (uint32_t base = 0; base < n; base += NG) {
@@ -138,31 +158,27 @@ __device__ __forceinline__ void run_groups(const uint2* ents, uint32_t n, uint32
     }
     const bool valid = g < b;
     const uint32_t slot = valid ? slots[p + g] : 0u;
-    float x[D];
-    if (valid) {
-      load_row<D>(r.x + (size_t)slot * r.dp, x);
-    } else {
-#pragma unroll
-      for (int k = 0; k < D; ++k) x[k] = 0.0f;
-    }
     float nrm = valid ? r.nrm[slot] : 0.0f;
     uint32_t cnt = valid ? r.cnt[slot] : 0u;
     uint32_t hd = valid ? r.head[slot] : 0u;
     const uint32_t tl = valid ? r.tail[slot] : 0u;
-#pragma unroll
-    for (int k = 0; k < D; k += 4)
-      *reinterpret_cast<float4*>(myrow + k) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
+    stage_rows<D>(r.x, r.dp, slot, valid, lds);  // row of lane l -> LDS row l, coalesced
     lds_fence();
+    float x[D];
+    load_row<D>(myrow, x);
     const uint32_t bmax = wave_max(b);
 
     // 1. every pairwise decision of the run.  decide(a, c) == decide(c, a): the products, their
     //    summation order and the sqrt product are the same either way.
     uint64_t full = 0ull;
-    for (uint32_t j = 0; j + 1 < bmax; ++j) {
-      const float nj = shflf(nrm, gbase + j);
+    for (uint32_t j = 0; j + 1 < bmax; j += 2) {  // two candidates per step: independent chains
+      const uint32_t j1 = (j + 1 < (uint32_t)G) ? j + 1 : j;
+      const float nj0 = shflf(nrm, gbase + j), nj1 = shflf(nrm, gbase + j1);
       if (valid && g > j) {
-        const float dot = dot_reg_lds<D>(x, lds + (gbase + j) * ST);
-        if (cos_decide(dot, nrm, nj, thr)) full |= 1ull << j;
+        float d0, d1;
+        dot2_reg_lds<D>(x, lds + (gbase + j) * ST, lds + (gbase + j1) * ST, d0, d1);
+        if (cos_decide(d0, nrm, nj0, thr)) full |= 1ull << j;
+        if (g > j + 1 && cos_decide(d1, nrm, nj1, thr)) full |= 1ull << (j + 1);
       }
     }
     for (uint32_t c = 1; c < bmax; ++c) {
