@@ -129,7 +129,8 @@ struct klsh_ctx {
     dfree(rows.x); dfree(rows.nrm); dfree(rows.cnt); dfree(rows.head); dfree(rows.tail);
     dfree(rows.nxt); dfree(order); dfree(alt); dfree(keys); dfree(keys2); dfree(nk1);
     dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.seg); dfree(mw.over);
-    dfree(mw.big); dfree(mw.huge);
+    dfree(mw.huge);
+    for (auto& c : mw.big) dfree(c);
     for (auto& c : mw.cls) dfree(c);
     cap_slots = cap_members = 0;
     cap_dp = 0;
@@ -176,7 +177,8 @@ struct klsh_ctx {
         (e = dalloc(&hist, 256 * ((s + klsh::kRadixTile - 1) / klsh::kRadixTile) + 256)) ||
         (e = dalloc(&tile_sums, (256 * s) / klsh::kScanTile + 1024)) ||
         (e = dalloc(&mw.seg, s + 64)) || (e = dalloc(&mw.over, s + 64)) ||
-        (e = dalloc(&mw.big, s / 65 + 64)) || (e = dalloc(&mw.huge, s / (klsh::kBigRows + 1) + 64))) {
+        (e = dalloc(&mw.big[0], s / 65 + 64)) || (e = dalloc(&mw.big[1], s / 129 + 64)) ||
+        (e = dalloc(&mw.big[2], s / 385 + 64)) || (e = dalloc(&mw.huge, s / 897 + 64))) {
       release_state();
       return e;
     }

@@ -13,10 +13,11 @@ constexpr int kMaxHyperplanes = 32;         // keys are uint32 (h = floor(log2 N
 constexpr int kRadixTile = 2048;            // keys per radix-sort workgroup (256 lanes x 8 rounds)
 constexpr int kScanTile = 4096;             // items per scan workgroup (256 lanes x 16)
 
-// Bucket runs longer than 64 rows and up to kBigRows rows are merged by one workgroup with the
-// run in LDS (k_merge_big); longer runs by one wave from memory (k_merge_wave).
-constexpr int kBigRows = 384;
-constexpr int kBigWords = kBigRows / 64;
+// Bucket runs of 65..896 rows are merged by one workgroup with the run's decision matrix in LDS
+// (k_merge_big; three size classes, rows in LDS up to 384); longer runs by one wave from memory
+// (k_merge_wave).
+constexpr int kBigClasses = 3;
+constexpr int kBigRows[kBigClasses] = {128, 384, 896};
 
 // Runs of 2..64 rows are merged by G-lane groups, one size class per G = 2, 4, ..., 64
 // (class c holds runs of 2^c < b <= 2^(c+1) rows).
@@ -27,18 +28,18 @@ inline uint64_t group_class_capacity(int c, uint64_t cap) { return cap / ((1ull 
 struct Counters {
   uint32_t n_seg;                  // bucket runs found by the segment scan
   uint32_t n_cls[kGroupClasses];   // runs of 2..64 rows queued per size class
-  uint32_t n_big;                  // runs of 65..kBigRows rows queued for k_merge_big
-  uint32_t n_huge;                 // runs longer than kBigRows queued for k_merge_wave
+  uint32_t n_big[kBigClasses];     // runs of 65..896 rows queued for k_merge_big, per class
+  uint32_t n_huge;                 // longer runs queued for k_merge_wave
   uint32_t n_over;                 // runs longer than bucket_size_threshold (nestedCluster)
   uint32_t total;                  // result of the last scan/compaction (live rows)
-  uint32_t pad[5];
+  uint32_t pad[3];
 };
 
 // Merge workspace (device), sized for `cap` positions.
 struct MergeWork {
   uint32_t* seg;                   // run starts [n_seg]
   uint2* cls[kGroupClasses];       // (start, length) of runs per size class
-  uint2* big;                      // (start, length) of runs for k_merge_big
+  uint2* big[kBigClasses];         // (start, length) of runs for k_merge_big, per class
   uint2* huge;                     // (start, length) of runs for k_merge_wave
   uint2* over;                     // (start, length) of oversize runs
   uint32_t* tile_sums;

@@ -16,10 +16,10 @@
 //                   at once (each an exact sequential fp32 dot product; decisions are
 //                   symmetric), then replays the walk on the decision bits; after a merge only
 //                   the decisions of rows still to be visited against the new row are redone.
-//   k_merge_big     one workgroup per run of 65..kBigRows rows: the same scheme with the run's
-//                   rows and its decision matrix in LDS, kept in POSITION space so every step of
-//                   the walk is a few bit operations.
-//   k_merge_wave    runs longer than kBigRows: one wave per run, the reference order directly.
+//   k_merge_big     one workgroup per run of 65..896 rows: the same scheme with the run's
+//                   decision matrix (and rows, up to 384) in LDS, kept in POSITION space so
+//                   every step of the walk is a few bit operations.
+//   k_merge_wave    longer runs: one wave per run, the reference order directly.
 //
 // Results are positional (survivors in place, kInvalid after), so they do not depend on which
 // wave handled which run or in what order.
@@ -127,8 +127,9 @@ __device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucke
                                                const MergeWork& w, Counters* ctr) {
   if (bucket_thr >= 0 && b > (uint32_t)bucket_thr) {  // cluster.cc:286 -> nestedCluster
     w.over[atomicAdd(&ctr->n_over, 1u)] = make_uint2(p, b);
-  } else if (b <= (uint32_t)kBigRows) {
-    w.big[atomicAdd(&ctr->n_big, 1u)] = make_uint2(p, b);
+  } else if (b <= (uint32_t)kBigRows[kBigClasses - 1]) {
+    const int c = b <= (uint32_t)kBigRows[0] ? 0 : b <= (uint32_t)kBigRows[1] ? 1 : 2;
+    w.big[c][atomicAdd(&ctr->n_big[c], 1u)] = make_uint2(p, b);
   } else {
     w.huge[atomicAdd(&ctr->n_huge, 1u)] = make_uint2(p, b);
   }
@@ -186,21 +187,31 @@ __device__ __forceinline__ void run_groups(const uint2* ents, uint32_t n, uint32
       if (c > g && ((mc >> g) & 1ull)) full |= 1ull << c;
     }
 
-    // 2. replay the walk on the bits
+    // 2. replay the walk on the bits.  Positions that find no candidate below them change
+    //    nothing, so each round jumps straight to the first position q >= i whose row matches
+    //    some row at a position below q (exclusive prefix-OR of row bits over positions).
     uint32_t rowid = g;  // row id at my position
     uint32_t mypos = g;  // position of my row
     bool alive = valid, dirty = false;
     uint32_t i = 1, size = b;  // uniform within the group
     while (true) {
-      const bool active = i < size;
-      if (__ballot(active) == 0ull) break;
-      const uint32_t ic = active ? i : 0u;
-      const uint32_t rr = shfl32(rowid, gbase + ic);  // row being visited (the reference's i)
-      const uint64_t fr = shfl64(full, gbase + rr);
-      const bool hit = active && g < i && ((fr >> rowid) & 1ull);
+      const uint64_t mybit = g < size ? (1ull << rowid) : 0ull;
+      uint64_t incl = mybit;
+#pragma unroll
+      for (uint32_t o = 1; o < (uint32_t)G; o <<= 1) {
+        const uint64_t y = shfl64(incl, lane >= o ? lane - o : lane);
+        if (g >= o) incl |= y;
+      }
+      const uint64_t frow = shfl64(full, gbase + rowid);  // decisions of the row at my position
+      const bool hit = g >= i && g < size && (frow & (incl & ~mybit)) != 0ull;
       const uint64_t m = __ballot(hit) & gmask;
+      if (__ballot(m != 0ull) == 0ull) break;  // every group of the wave is done
       if (m != 0ull) {
-        const uint32_t jpos = (uint32_t)(__ffsll((unsigned long long)m) - 1) - gbase;
+        i = (uint32_t)(__ffsll((unsigned long long)m) - 1) - gbase;  // the reference's i
+        const uint32_t rr = shfl32(rowid, gbase + i);
+        const uint64_t fr = shfl64(frow, gbase + i);
+        const uint64_t mj = __ballot(g < i && ((fr >> rowid) & 1ull)) & gmask;
+        const uint32_t jpos = (uint32_t)(__ffsll((unsigned long long)mj) - 1) - gbase;
         const uint32_t c = shfl32(rowid, gbase + jpos);  // first matching candidate (row j)
         const uint32_t ca = shfl32(cnt, gbase + rr), cb = shfl32(cnt, gbase + c);
         const uint32_t hr = shfl32(hd, gbase + rr), tr = shfl32(tl, gbase + rr);
@@ -237,8 +248,6 @@ __device__ __forceinline__ void run_groups(const uint2* ents, uint32_t n, uint32
           const float dot = dot_reg_lds<D>(x, rowc);
           full = cos_decide(dot, nrm, nc, thr) ? (full | (1ull << c)) : (full & ~(1ull << c));
         }
-      } else if (active) {
-        ++i;
       }
     }
 
@@ -309,45 +318,49 @@ __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ li
     run_groups<G, D>(list + bi * NG, min(NG, n - bi * NG), slots, thr, r, lds);
 }
 
-// ----------------------------------------------------------------- runs of 65..kBigRows -----
-// One workgroup (4 waves) per run; the run's rows, norms, member bookkeeping and its decision
-// matrix live in LDS.  The matrix is kept in POSITION space: P[y] bit q = decide(row y, row at
-// position q), so the walk's "first j < i" is a find-first-set over <= kBigWords words.
-template <int D>
+// ------------------------------------------------------------------- runs of 65..896 rows -----
+// One workgroup per run.  The run's metadata and its decision matrix live in LDS, the rows too
+// when they fit (ROWS_LDS; otherwise they are read from memory, L2-resident, and staged one
+// 64-row column block at a time for the decision phase).  The matrix is kept in POSITION space:
+// P[y] bit q = decide(row y, row at position q), so the walk's "first j < i" is a
+// find-first-set over W words, and positions that find nothing are skipped in bulk.
+template <int D, int RB, bool ROWS_LDS>
 struct BigLayout {
   static constexpr int ST = D + 4;
-  static constexpr int W = kBigWords;
+  static constexpr int W = RB / 64;
   static constexpr size_t rows = 0;
-  static constexpr size_t P = rows + sizeof(float) * kBigRows * ST;
-  static constexpr size_t Q = P + sizeof(uint64_t) * kBigRows * W;
-  static constexpr size_t meta = Q + sizeof(uint64_t) * kBigRows * W;
-  static constexpr size_t bytes = meta + sizeof(uint32_t) * kBigRows * 6;
+  static constexpr size_t P = rows + sizeof(float) * ST * (ROWS_LDS ? RB : 64);
+  static constexpr size_t meta = P + sizeof(uint64_t) * RB * W;
+  static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 6;
 };
 
-template <int D>
-__global__ __launch_bounds__(256) void k_merge_big(const uint2* __restrict__ list,
-                                                   uint32_t* __restrict__ slots, float thr, Rows r,
-                                                   Counters* ctr) {
-  using L = BigLayout<D>;
-  constexpr int ST = L::ST, W = L::W;
+template <int D, int RB, int NT, bool ROWS_LDS>
+__global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list, int cls,
+                                                  uint32_t* __restrict__ slots, float thr, Rows r,
+                                                  Counters* ctr) {
+  using L = BigLayout<D, RB, ROWS_LDS>;
+  constexpr int ST = L::ST, W = L::W, NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* rows = reinterpret_cast<float*>(smem + L::rows);
+  float* rows = reinterpret_cast<float*>(smem + L::rows);  // rows, or one staged column block
   uint64_t* P = reinterpret_cast<uint64_t*>(smem + L::P);  // [row][W] position-space masks
-  uint64_t* Q = reinterpret_cast<uint64_t*>(smem + L::Q);  // [row][W] decisions vs later rows
   uint32_t* slot = reinterpret_cast<uint32_t*>(smem + L::meta);
-  float* nrm = reinterpret_cast<float*>(slot + kBigRows);
-  uint32_t* cnt = slot + 2 * kBigRows;
-  uint32_t* hd = slot + 3 * kBigRows;
-  uint32_t* tl = slot + 4 * kBigRows;
-  uint32_t* pos2row = slot + 5 * kBigRows;
+  float* nrm = reinterpret_cast<float*>(slot + RB);
+  uint32_t* cnt = slot + 2 * RB;
+  uint32_t* hd = slot + 3 * RB;
+  uint32_t* tl = slot + 4 * RB;
+  uint32_t* pos2row = slot + 5 * RB;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t count = __hip_atomic_load(&ctr->n_big, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t count =
+      __hip_atomic_load(&ctr->n_big[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto row_ptr = [&](uint32_t a) -> const float* {
+    return ROWS_LDS ? rows + a * ST : r.x + (size_t)slot[a] * r.dp;
+  };
 
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
     const uint2 e = list[li];
     const uint32_t p = e.x, b = e.y;
-    // load the run
-    for (uint32_t a = t; a < b; a += 256) {
+    const uint32_t nblk = (b + 63) / 64;
+    for (uint32_t a = t; a < b; a += NT) {
       const uint32_t s = slots[p + a];
       slot[a] = s;
       nrm[a] = r.nrm[s];
@@ -356,55 +369,99 @@ __global__ __launch_bounds__(256) void k_merge_big(const uint2* __restrict__ lis
       tl[a] = r.tail[s];
       pos2row[a] = a;
     }
-    for (uint32_t a = t; a < (uint32_t)kBigRows * W; a += 256) {
-      P[a] = 0ull;
-      Q[a] = 0ull;
-    }
+    for (uint32_t a = t; a < b * (uint32_t)W; a += NT) P[a] = 0ull;
     __syncthreads();
-    for (uint32_t q = t; q < b * (uint32_t)(D / 4); q += 256) {
-      const uint32_t a = q / (D / 4), k = (q % (D / 4)) * 4;
-      *reinterpret_cast<float4*>(rows + a * ST + k) =
-          *reinterpret_cast<const float4*>(r.x + (size_t)slot[a] * r.dp + k);
+    if constexpr (ROWS_LDS) {
+      for (uint32_t q = t; q < b * (uint32_t)(D / 4); q += NT) {
+        const uint32_t a = q / (D / 4), k = (q % (D / 4)) * 4;
+        *reinterpret_cast<float4*>(rows + a * ST + k) =
+            *reinterpret_cast<const float4*>(r.x + (size_t)slot[a] * r.dp + k);
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    // decisions: thread a (row-stationary) against every earlier row c; at step c the wave's
-    // lanes all read row c (LDS broadcast) and the wave's ballot is P[c]'s word for its rows.
-    for (uint32_t a0 = wv * 64; a0 < b; a0 += 256) {
-      const uint32_t a = a0 + lane;
+
+    // decisions in 64x64 tiles (row block R, column block C <= R): lanes = rows of R with the
+    // row in registers, columns walked in order (LDS broadcast); the wave's ballot at column c
+    // is P[c]'s word R, the lane's own bits form P[a]'s word C.
+    auto tile = [&](uint32_t R, uint32_t C, const float* colrows) {
+      const uint32_t a = R * 64u + lane;
       float xa[D];
       if (a < b) {
-        load_row<D>(rows + a * ST, xa);
+        load_row<D>(row_ptr(a), xa);
       } else {
 #pragma unroll
         for (int k = 0; k < D; ++k) xa[k] = 0.0f;
       }
       const float na = a < b ? nrm[a] : 0.0f;
-      uint64_t own[W];
-#pragma unroll
-      for (int k = 0; k < W; ++k) own[k] = 0ull;
-      const uint32_t cend = min(b, a0 + 64u) - 1;  // last row any lane of this wave needs
-      for (uint32_t c = 0; c < cend; ++c) {
-        bool dc = false;
-        if (a < b && c < a) dc = cos_decide(dot_reg_lds<D>(xa, rows + c * ST), na, nrm[c], thr);
-        const uint64_t m = __ballot(dc);  // rows a0..a0+63 that match row c
-        if (lane == 0) Q[c * W + a0 / 64] = m;
-#pragma unroll
-        for (int k = 0; k < W; ++k)
-          if ((uint32_t)k == c / 64 && dc) own[k] |= 1ull << (c & 63u);
+      uint64_t own = 0ull;
+      const uint32_t c0 = C * 64u, c1 = min(b, c0 + 64u);
+      for (uint32_t c = c0; c < c1; c += 2) {
+        const uint32_t cb = (c + 1 < c1) ? c + 1 : c;
+        float d0, d1;
+        dot2_reg_lds<D>(xa, colrows + (c - c0) * ST, colrows + (cb - c0) * ST, d0, d1);
+        const bool h0 = a < b && c < a && cos_decide(d0, na, nrm[c], thr);
+        const bool h1 = a < b && c + 1 < c1 && c + 1 < a && cos_decide(d1, na, nrm[cb], thr);
+        const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
+        if (lane == 0) {
+          if (m0) atomicOr((unsigned long long*)&P[c * W + R], (unsigned long long)m0);
+          if (m1) atomicOr((unsigned long long*)&P[cb * W + R], (unsigned long long)m1);
+        }
+        own |= (h0 ? 1ull : 0ull) << (c - c0);
+        if (c + 1 < c1) own |= (h1 ? 1ull : 0ull) << (c + 1 - c0);
       }
-      if (a < b) {
-#pragma unroll
-        for (int k = 0; k < W; ++k) P[a * W + k] = own[k];
+      if (a < b && own) atomicOr((unsigned long long*)&P[a * W + C], (unsigned long long)own);
+    };
+    if constexpr (ROWS_LDS) {
+      const uint32_t ntiles = nblk * (nblk + 1) / 2;
+      for (uint32_t ti = wv; ti < ntiles; ti += NW) {
+        uint32_t R = 0;
+        while ((R + 1) * (R + 2) / 2 <= ti) ++R;
+        const uint32_t C = ti - R * (R + 1) / 2;
+        tile(R, C, rows + C * 64u * ST);
+      }
+    } else {
+      for (uint32_t C = 0; C < nblk; ++C) {
+        for (uint32_t q = t; q < 64u * (uint32_t)(D / 4); q += NT) {
+          const uint32_t a = C * 64u + q / (D / 4), k = (q % (D / 4)) * 4;
+          if (a < b)
+            *reinterpret_cast<float4*>(rows + (a - C * 64u) * ST + k) =
+                *reinterpret_cast<const float4*>(r.x + (size_t)slot[a] * r.dp + k);
+        }
+        __syncthreads();
+        for (uint32_t R = C + wv; R < nblk; R += NW) tile(R, C, rows);
+        __syncthreads();
       }
     }
     __syncthreads();
-    for (uint32_t a = t; a < b * (uint32_t)W; a += 256) P[a] |= Q[a];  // symmetric
-    __syncthreads();
 
-    // the walk, by wave 0
+    // the walk, by wave 0: jump to the first position q >= i whose row matches a position
+    // below q (positions that find nothing change nothing), then do the reference's merge there.
     if (wv == 0) {
       uint32_t i = 1, size = b;
-      while (i < size) {
+      while (true) {
+        uint32_t q = size;
+        for (uint32_t q0 = i; q0 < size; q0 += 64) {
+          const uint32_t qq = q0 + lane;
+          bool hit = false;
+          if (qq < size) {
+            const uint64_t* Py = P + pos2row[qq] * W;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+              const uint32_t lo = (uint32_t)k * 64u;
+              if (lo < qq) {
+                const uint64_t wk = Py[k];
+                hit |= (qq - lo >= 64u ? wk : (wk & ((1ull << (qq - lo)) - 1ull))) != 0ull;
+              }
+            }
+          }
+          const uint64_t m = __ballot(hit);
+          if (m != 0ull) {
+            q = q0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+            break;
+          }
+        }
+        if (q >= size) break;
+        i = q;
         const uint32_t rr = pos2row[i];
         // first position j < i with P[rr] bit j
         uint64_t word = 0ull;
@@ -415,25 +472,21 @@ __global__ __launch_bounds__(256) void k_merge_big(const uint2* __restrict__ lis
           else if (i - lo < 64u) word &= (1ull << (i - lo)) - 1ull;
         }
         const uint64_t nz = __ballot(word != 0ull);
-        if (nz == 0ull) {
-          ++i;
-          continue;
-        }
         const uint32_t wd = (uint32_t)(__ffsll((unsigned long long)nz) - 1);
         const uint64_t wbits = shfl64(word, wd);
         const uint32_t j = wd * 64u + (uint32_t)(__ffsll((unsigned long long)wbits) - 1);
         const uint32_t c = pos2row[j];
         const uint32_t ca = cnt[rr], cb = cnt[c];
         const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
-        float* rowc = rows + c * ST;
-        const float* rowr = rows + rr * ST;
         float* xc = r.x + (size_t)slot[c] * r.dp;
+        float* rowc = ROWS_LDS ? rows + c * ST : xc;
+        const float* rowr = row_ptr(rr);
         for (int k = (int)lane; k < D; k += 64) {
           const float v = consensus(rowr[k], fa, rowc[k], fb, fn);
-          rowc[k] = v;
+          if (ROWS_LDS) rowc[k] = v;
           xc[k] = v;
         }
-        lds_fence();
+        lds_fence();  // workgroup-scope fence: LDS and global stores of this wave
         if (lane == 0) {
           float nn = 0.0f;
           for (int k = 0; k < D; ++k) nn = nn + rowc[k] * rowc[k];
@@ -448,14 +501,17 @@ __global__ __launch_bounds__(256) void k_merge_big(const uint2* __restrict__ lis
         --size;
         const float nc = nrm[c];
         const uint32_t moved = size;  // old position of the row now at i
-        for (uint32_t q = i + lane; q < size; q += 64) {  // rows still to be visited
-          const uint32_t y = pos2row[q];
+        for (uint32_t qq = i + lane; qq < size; qq += 64) {  // rows still to be visited
+          const uint32_t y = pos2row[qq];
           uint64_t* Py = P + y * W;
           // the row that sat at position `moved` is now at position i
           const bool bm = (Py[moved / 64] >> (moved & 63u)) & 1ull;
           Py[moved / 64] &= ~(1ull << (moved & 63u));
           Py[i / 64] = bm ? (Py[i / 64] | (1ull << (i & 63u))) : (Py[i / 64] & ~(1ull << (i & 63u)));
-          const bool dn = cos_decide(dot_lds_lds<D>(rows + y * ST, rowc), nrm[y], nc, thr);
+          float dot;
+          if constexpr (ROWS_LDS) dot = dot_lds_lds<D>(row_ptr(y), rowc);
+          else dot = dot_mem_mem(row_ptr(y), rowc, D);
+          const bool dn = cos_decide(dot, nrm[y], nc, thr);
           Py[j / 64] = dn ? (Py[j / 64] | (1ull << (j & 63u))) : (Py[j / 64] & ~(1ull << (j & 63u)));
         }
         lds_fence();
@@ -610,6 +666,21 @@ __global__ __launch_bounds__(256) void k_merge_lane_generic(const uint32_t* __re
 }
 
 // ----------------------------------------------------------------------------- launch -----
+template <int D, int RB, int NT, bool ROWS_LDS>
+static void launch_big(const MergeWork& w, int c, uint32_t* slots, float thr, const Rows& r,
+                       Counters* ctr, uint32_t n, hipStream_t s) {
+  using L = BigLayout<D, RB, ROWS_LDS>;
+  static const bool lds_ok = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_big<D, RB, NT, ROWS_LDS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)L::bytes) == hipSuccess;
+  }();
+  (void)lds_ok;
+  const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
+  const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
+  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, thr, r, ctr);
+}
+
 template <int D>
 static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
                           uint32_t* slots, float thr, const MergeWork& w, Counters* ctr,
@@ -625,15 +696,10 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   k_merge_group<16, D><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, thr, r, ctr);
   k_merge_group<32, D><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, thr, r, ctr);
   k_merge_group<64, D><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, thr, r, ctr);
-  static bool lds_ok = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_big<D>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)BigLayout<D>::bytes) == hipSuccess;
-  }();
-  (void)lds_ok;
-  const uint32_t g2 = (uint32_t)std::min<uint64_t>(1024, n / 65 + 1);
-  k_merge_big<D><<<g2, 256, BigLayout<D>::bytes, s>>>(w.big, slots, thr, r, ctr);
-  const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows + 1) + 1);
+  launch_big<D, 128, 128, true>(w, 0, slots, thr, r, ctr, n, s);
+  launch_big<D, 384, 256, true>(w, 1, slots, thr, r, ctr, n, s);
+  launch_big<D, 896, 256, false>(w, 2, slots, thr, r, ctr, n, s);
+  const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 1] + 1) + 1);
   k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, thr, r);
 }
 

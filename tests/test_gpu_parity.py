@@ -77,6 +77,8 @@ def test_pcluster_matches_reference(engine, name):
 @pytest.mark.parametrize("b,d,groups,noise,thr", [
     (65, 64, 6, 0.05, 0.9), (200, 32, 12, 0.08, 0.85), (384, 64, 30, 0.05, 0.95),
     (385, 64, 30, 0.05, 0.95), (700, 16, 50, 0.1, 0.8), (64, 8, 3, 0.2, 0.9), (3, 64, 1, 0.01, 0.9),
+    (128, 64, 10, 0.05, 0.9), (129, 64, 10, 0.05, 0.9), (896, 64, 200, 0.05, 0.95),
+    (897, 32, 200, 0.05, 0.95), (600, 8, 40, 0.1, 0.85), (250, 16, 1, 0.0, 0.9),
 ])
 def test_pcluster_run_lengths_vs_oracle(engine, oracle, b, d, groups, noise, thr):
     """Every merge path by bucket length: G-lane groups (<= 64), LDS matrix (65..384), wave (> 384)."""
