@@ -79,6 +79,31 @@ def max_over_ranks(world, value: float) -> float:
     return float(t.item())
 
 
+def device_sync(local: int) -> None:
+    """torch.cuda.synchronize() (the engine already syncs its own stream before returning)."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.synchronize(local)
+
+
+def timed(step, steps: int, warmup: int, world: int, local: int = 0, sync=device_sync):
+    """W untimed steps, then exactly K steps bracketed by barrier + device sync on both sides;
+    returns (max over ranks of the elapsed seconds, the K step results)."""
+    for _ in range(warmup):
+        step()
+    sync(local)
+    barrier(world)
+    t0 = time.perf_counter()
+    results = [step() for _ in range(steps)]
+    sync(local)
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    return max_over_ranks(world, elapsed), results
+
+
 def prepare(eng, n, d, seed):
     """synth counts -> GPU convert -> init pass; returns (rng counter, kept rows, init stats)."""
     from kmerlsh_amd import _native
@@ -184,16 +209,8 @@ def main():
         _, _, st = eng.cluster(min_sim, iters, 1_000_000, 12345, counter0)
         return st
 
-    for w in range(args.warmup):
-        st = step()
-        log(f"warmup {w}: {st['wall_ms']:.1f} ms, {st['iterations']} iterations, "
-            f"final {st['n_final']} clusters")
-    barrier(world)
-    t0 = time.perf_counter()
-    stats = [step() for _ in range(args.steps)]
-    barrier(world)
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(world, elapsed)
+    elapsed, stats = timed(step, args.steps, args.warmup, world, local)
+    log(f"{args.steps} timed steps: {elapsed:.3f} s (max over {world} ranks)")
 
     if rank != 0:
         return
@@ -213,7 +230,8 @@ def main():
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 5),
-        "traffic": traffic,
+        "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+        "traffic_source": (traffic or {}).get("source"),
         "bytes_per_launch": proj_bytes / max(1, launches),
         "avg_launch_ms": avg_ms,
         "launches_per_step": launches / args.steps,
