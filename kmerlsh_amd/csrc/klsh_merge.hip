@@ -138,27 +138,20 @@ __device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucke
 // --------------------------------------------------------------------- G-lane groups -----
 // The wave handles n runs listed in LDS (ents), 64/G at a time.  Lane g of a group is position
 // g of its run and owns row id g: row in registers x[] and at LDS row `lane`.
+// One batch: run (p, b) of lane's group, lane's slot already loaded (the caller pipelines those
+// loads one batch ahead, so only the row gather is exposed here).
 template <int G, int D>
-__device__ __forceinline__ void run_groups(const uint2* ents, uint32_t n, uint32_t* slots,
-                                           float thr, const Rows& r, float* lds) {
-  constexpr uint32_t NG = 64 / G;
+__device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
+                                            uint32_t* slots, float thr, const Rows& r,
+                                            float* lds) {
   constexpr int ST = D + 4;  // padded row stride: 16 lanes of a ds_read_b128 hit distinct banks
   const uint32_t lane = threadIdx.x;
   const uint32_t g = lane & (G - 1);
   const uint32_t gbase = lane - g;
   const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << (G & 63)) - 1ull) << gbase);
   float* myrow = lds + lane * ST;
-
-  for (uint32_t base = 0; base < n; base += NG) {
-    const uint32_t bi = base + lane / G;
-    uint32_t p = 0, b = 0;
-    if (bi < n) {
-      const uint2 e = ents[bi];
-      p = e.x;
-      b = e.y;
-    }
+  {
     const bool valid = g < b;
-    const uint32_t slot = valid ? slots[p + g] : 0u;
     float nrm = valid ? r.nrm[slot] : 0.0f;
     uint32_t cnt = valid ? r.cnt[slot] : 0u;
     uint32_t hd = valid ? r.head[slot] : 0u;
@@ -306,6 +299,8 @@ __global__ __launch_bounds__(1024) void k_classify(const uint32_t* __restrict__ 
 }
 
 // One wave per batch of 64/G runs of one size class (persistent over the class list).
+// One wave per batch of 64/G runs of one size class (persistent over the class list).  The list
+// entry and the slots of the NEXT batch are loaded while the current one is merged.
 template <int G, int D>
 __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ list, int cls,
                                                     uint32_t* __restrict__ slots, float thr,
@@ -314,8 +309,22 @@ __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ li
   constexpr uint32_t NG = 64 / G;
   const uint32_t n = __hip_atomic_load(&ctr->n_cls[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nb = (n + NG - 1) / NG;
-  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x)
-    run_groups<G, D>(list + bi * NG, min(NG, n - bi * NG), slots, thr, r, lds);
+  const uint32_t g = threadIdx.x & (G - 1), grp = threadIdx.x / G;
+  auto entry = [&](uint32_t bi) -> uint2 {
+    const uint32_t k = bi * NG + grp;
+    return (bi < nb && k < n) ? list[k] : make_uint2(0u, 0u);
+  };
+  uint2 e = entry(blockIdx.x);
+  uint32_t slot = g < e.y ? slots[e.x + g] : 0u;
+  uint2 e_next = entry(blockIdx.x + gridDim.x);
+  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
+    const uint32_t slot_next = g < e_next.y ? slots[e_next.x + g] : 0u;
+    const uint2 e_next2 = entry(bi + 2 * gridDim.x);
+    merge_batch<G, D>(e.x, e.y, slot, slots, thr, r, lds);
+    e = e_next;
+    slot = slot_next;
+    e_next = e_next2;
+  }
 }
 
 // ------------------------------------------------------------------- runs of 65..896 rows -----
