@@ -10,13 +10,16 @@ namespace klsh {
 // ============================================================================ helpers ==========
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-// The merge test of cluster.cc:68-69 given the exact sequential dot product and the cached
-// sequential norms: sim = dot / (sqrtf(|a|^2) * sqrtf(|b|^2)); dist = 1 - sim; 1 - dist >= thr.
-__device__ __forceinline__ bool cos_decide(float dot, float ni, float nj, float thr) {
-  const float den = __builtin_sqrtf(ni) * __builtin_sqrtf(nj);
-  const float sim = dot / den;
-  const float dist = 1.0f - sim;
-  return (1.0f - dist) >= thr;
+// The merge test of cluster.cc:68-69 given the exact sequential dot product and
+// den = sqrtf(|a|^2) * sqrtf(|b|^2) (each sqrt correctly rounded, cached per row): see Decider.
+__device__ __forceinline__ bool decide(const Decider& dc, float dot, float den) {
+  if (dc.fast) {
+    const bool den_ok = den >= 0x1p-100f && den <= 0x1p100f;  // rcp(den) normal, no flush
+    const float q = dot * __builtin_amdgcn_rcpf(den);
+    if (den_ok && q >= dc.s_hi) return true;
+    if (den_ok && q <= dc.s_lo) return false;
+  }
+  return dot / den >= dc.s_star;  // correctly rounded quotient; NaN never merges
 }
 
 // Consensus element (funcAB.cc:65): v1*c1/n + v2*c2/n, each op rounded, current row first.

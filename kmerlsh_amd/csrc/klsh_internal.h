@@ -58,6 +58,19 @@ struct Rows {
   int dp;
 };
 
+// The merge test of cluster.cc:68-69 as a threshold on the quotient.  The reference computes
+// sim = dot / (sqrtf(|a|^2) * sqrtf(|b|^2)); dist = 1 - sim; and merges when 1 - dist >= thr.
+// s -> fl(1 - fl(1 - s)) is monotone in s, so the test is exactly fl(dot / den) >= s_star for the
+// smallest float s_star that passes (computed on the host by make_decider, NaN if none does).
+// Fast path (`fast` != 0, s_star a positive normal float): q = dot * rcp(den) is within 2 ulp of
+// dot / den, so q >= s_hi (s_star + 8 ulp) or q <= s_lo (s_star - 8 ulp) settles the test and only
+// quotients within a few ulp of s_star take the correctly rounded division.
+struct Decider {
+  float s_star, s_lo, s_hi;
+  uint32_t fast;
+};
+Decider make_decider(float thr);
+
 // ---- launch wrappers (all asynchronous on `s`) ------------------------------------------------
 // keys[p] = sign-hash of row slots[p] against h hyperplanes W (h x dp), OR'ed with key_or.
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,

@@ -24,6 +24,8 @@
 // Results are positional (survivors in place, kInvalid after), so they do not depend on which
 // wave handled which run or in what order.
 #include <algorithm>
+#include <cstring>
+#include <limits>
 
 #include "klsh_device.cuh"
 
@@ -142,7 +144,7 @@ __device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucke
 // loads one batch ahead, so only the row gather is exposed here).
 template <int G, int D>
 __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
-                                            uint32_t* slots, float thr, const Rows& r,
+                                            uint32_t* slots, const Decider& dc, const Rows& r,
                                             float* lds) {
   constexpr int ST = D + 4;  // padded row stride: 16 lanes of a ds_read_b128 hit distinct banks
   const uint32_t lane = threadIdx.x;
@@ -157,27 +159,41 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
     uint32_t hd = valid ? r.head[slot] : 0u;
     const uint32_t tl = valid ? r.tail[slot] : 0u;
     stage_rows<D>(r.x, r.dp, slot, valid, lds);  // row of lane l -> LDS row l, coalesced
+    float sq = __builtin_sqrtf(nrm);             // this row's sqrtf(|x|^2), distance.cc:37
     lds_fence();
     float x[D];
     load_row<D>(myrow, x);
     const uint32_t bmax = wave_max(b);
 
-    // 1. every pairwise decision of the run.  decide(a, c) == decide(c, a): the products, their
-    //    summation order and the sqrt product are the same either way.
+    // 1. every pairwise decision of the run, each unordered pair once: lane g pairs with the
+    //    rows k = 1 .. b/2 positions after it, cyclically.  decide(a, c) == decide(c, a) (same
+    //    products in the same order, the same sqrt product), so the partner receives the bit.
     uint64_t full = 0ull;
-    for (uint32_t j = 0; j + 1 < bmax; j += 2) {  // two candidates per step: independent chains
-      const uint32_t j1 = (j + 1 < (uint32_t)G) ? j + 1 : j;
-      const float nj0 = shflf(nrm, gbase + j), nj1 = shflf(nrm, gbase + j1);
-      if (valid && g > j) {
-        float d0, d1;
-        dot2_reg_lds<D>(x, lds + (gbase + j) * ST, lds + (gbase + j1) * ST, d0, d1);
-        if (cos_decide(d0, nrm, nj0, thr)) full |= 1ull << j;
-        if (g > j + 1 && cos_decide(d1, nrm, nj1, thr)) full |= 1ull << (j + 1);
+    const uint32_t half = b / 2;
+    auto partner = [&](uint32_t k) {  // (g + k) mod b, for k <= b
+      const uint32_t j = g + k;
+      return j >= b ? j - b : j;
+    };
+    auto share = [&](uint32_t k, bool bit) {  // bit = decide(g, g + k); give it to g + k
+      const uint32_t src = g >= k ? g - k : g + b - k;  // lane holding decide(src, g)
+      const uint32_t in = (uint32_t)__shfl((int)bit, (int)(gbase + (src & (G - 1))), 64);
+      if (valid && k <= half) {
+        full |= (uint64_t)bit << partner(k);
+        full |= (uint64_t)in << src;
       }
-    }
-    for (uint32_t c = 1; c < bmax; ++c) {
-      const uint64_t mc = shfl64(full, gbase + c);
-      if (c > g && ((mc >> g) & 1ull)) full |= 1ull << c;
+    };
+    for (uint32_t k = 1; k <= bmax / 2; k += 2) {  // two partners per step: independent chains
+      const uint32_t j0 = partner(min(k, b)), j1 = partner(min(k + 1, b));
+      const float s0 = shflf(sq, gbase + (j0 & (G - 1))), s1 = shflf(sq, gbase + (j1 & (G - 1)));
+      bool h0 = false, h1 = false;
+      if (valid && k <= half) {
+        float d0, d1;
+        dot2_reg_lds<D>(x, lds + (gbase + j0) * ST, lds + (gbase + j1) * ST, d0, d1);
+        h0 = decide(dc, d0, sq * s0);
+        h1 = k + 1 <= half && decide(dc, d1, sq * s1);
+      }
+      share(k, h0);
+      share(k + 1, h1);
     }
 
     // 2. replay the walk on the bits.  Positions that find no candidate below them change
@@ -220,12 +236,13 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
           xc[k] = v;
         }
         lds_fence();
-        if (g == c) {  // new row c: registers, exact sequential norm, member list head
-          load_row<D>(rowc, x);
-          float nn = 0.0f;
-#pragma unroll
-          for (int k = 0; k < D; ++k) nn = nn + x[k] * x[k];
-          nrm = nn;
+        // one pass: lane c (the new row c, reloaded) gets its exact sequential norm
+        // (distance.cc:33-34), every other lane the dot product of its row with row c
+        if (g == c) load_row<D>(rowc, x);
+        const float dot = dot_reg_lds<D>(x, rowc);
+        if (g == c) {
+          nrm = dot;
+          sq = __builtin_sqrtf(dot);
           cnt = ca + cb;
           hd = hr;
           dirty = true;
@@ -236,10 +253,9 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
         if (g == i) rowid = last;
         if (g == last) mypos = i;
         --size;
-        const float nc = shflf(nrm, gbase + c);
+        const float sc = shflf(sq, gbase + c);
         if (alive && mypos >= i && mypos < size) {  // rows still to be visited vs the new row c
-          const float dot = dot_reg_lds<D>(x, rowc);
-          full = cos_decide(dot, nrm, nc, thr) ? (full | (1ull << c)) : (full & ~(1ull << c));
+          full = decide(dc, dot, sq * sc) ? (full | (1ull << c)) : (full & ~(1ull << c));
         }
       }
     }
@@ -303,7 +319,7 @@ __global__ __launch_bounds__(1024) void k_classify(const uint32_t* __restrict__ 
 // entry and the slots of the NEXT batch are loaded while the current one is merged.
 template <int G, int D>
 __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ list, int cls,
-                                                    uint32_t* __restrict__ slots, float thr,
+                                                    uint32_t* __restrict__ slots, Decider dc,
                                                     Rows r, Counters* ctr) {
   __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
   constexpr uint32_t NG = 64 / G;
@@ -320,7 +336,7 @@ __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ li
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
     const uint32_t slot_next = g < e_next.y ? slots[e_next.x + g] : 0u;
     const uint2 e_next2 = entry(bi + 2 * gridDim.x);
-    merge_batch<G, D>(e.x, e.y, slot, slots, thr, r, lds);
+    merge_batch<G, D>(e.x, e.y, slot, slots, dc, r, lds);
     e = e_next;
     slot = slot_next;
     e_next = e_next2;
@@ -340,13 +356,13 @@ struct BigLayout {
   static constexpr size_t rows = 0;
   static constexpr size_t P = rows + sizeof(float) * ST * (ROWS_LDS ? RB : 64);
   static constexpr size_t meta = P + sizeof(uint64_t) * RB * W;
-  static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 6;
+  static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 7;
 };
 
 template <int D, int RB, int NT, bool ROWS_LDS>
 __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list, int cls,
-                                                  uint32_t* __restrict__ slots, float thr, Rows r,
-                                                  Counters* ctr) {
+                                                  uint32_t* __restrict__ slots, Decider dc,
+                                                  Rows r, Counters* ctr) {
   using L = BigLayout<D, RB, ROWS_LDS>;
   constexpr int ST = L::ST, W = L::W, NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -358,6 +374,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
   uint32_t* hd = slot + 3 * RB;
   uint32_t* tl = slot + 4 * RB;
   uint32_t* pos2row = slot + 5 * RB;
+  float* sq = reinterpret_cast<float*>(slot + 6 * RB);  // sqrtf(nrm), distance.cc:37
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t count =
       __hip_atomic_load(&ctr->n_big[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -373,6 +390,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
       const uint32_t s = slots[p + a];
       slot[a] = s;
       nrm[a] = r.nrm[s];
+      sq[a] = __builtin_sqrtf(nrm[a]);
       cnt[a] = r.cnt[s];
       hd[a] = r.head[s];
       tl[a] = r.tail[s];
@@ -401,15 +419,15 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
 #pragma unroll
         for (int k = 0; k < D; ++k) xa[k] = 0.0f;
       }
-      const float na = a < b ? nrm[a] : 0.0f;
+      const float sa = a < b ? sq[a] : 0.0f;
       uint64_t own = 0ull;
       const uint32_t c0 = C * 64u, c1 = min(b, c0 + 64u);
       for (uint32_t c = c0; c < c1; c += 2) {
         const uint32_t cb = (c + 1 < c1) ? c + 1 : c;
         float d0, d1;
         dot2_reg_lds<D>(xa, colrows + (c - c0) * ST, colrows + (cb - c0) * ST, d0, d1);
-        const bool h0 = a < b && c < a && cos_decide(d0, na, nrm[c], thr);
-        const bool h1 = a < b && c + 1 < c1 && c + 1 < a && cos_decide(d1, na, nrm[cb], thr);
+        const bool h0 = a < b && c < a && decide(dc, d0, sa * sq[c]);
+        const bool h1 = a < b && c + 1 < c1 && c + 1 < a && decide(dc, d1, sa * sq[cb]);
         const uint64_t m0 = __ballot(h0), m1 = __ballot(h1);
         if (lane == 0) {
           if (m0) atomicOr((unsigned long long*)&P[c * W + R], (unsigned long long)m0);
@@ -500,6 +518,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
           float nn = 0.0f;
           for (int k = 0; k < D; ++k) nn = nn + rowc[k] * rowc[k];
           nrm[c] = nn;
+          sq[c] = __builtin_sqrtf(nn);
           r.nxt[tl[rr]] = hd[c];  // ids_current ++ ids_candidate
           hd[c] = hd[rr];
           cnt[c] = ca + cb;
@@ -508,7 +527,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
         }
         lds_fence();
         --size;
-        const float nc = nrm[c];
+        const float sc = sq[c];
         const uint32_t moved = size;  // old position of the row now at i
         for (uint32_t qq = i + lane; qq < size; qq += 64) {  // rows still to be visited
           const uint32_t y = pos2row[qq];
@@ -520,7 +539,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
           float dot;
           if constexpr (ROWS_LDS) dot = dot_lds_lds<D>(row_ptr(y), rowc);
           else dot = dot_mem_mem(row_ptr(y), rowc, D);
-          const bool dn = cos_decide(dot, nrm[y], nc, thr);
+          const bool dn = decide(dc, dot, sq[y] * sc);
           Py[j / 64] = dn ? (Py[j / 64] | (1ull << (j & 63u))) : (Py[j / 64] & ~(1ull << (j & 63u)));
         }
         lds_fence();
@@ -544,7 +563,8 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
 template <int D>
 __global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ list,
                                                    const uint32_t* count_ptr,
-                                                   uint32_t* __restrict__ slots, float thr, Rows r) {
+                                                   uint32_t* __restrict__ slots, Decider dc,
+                                                   Rows r) {
   extern __shared__ __attribute__((aligned(16))) float sx[];  // consensus row for the norm
   const uint32_t lane = threadIdx.x;
   const uint32_t count = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -557,7 +577,7 @@ __global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ lis
     while (i < size) {
       const uint32_t si = s[i];
       const float* xip = r.x + (size_t)si * r.dp;
-      const float ni = r.nrm[si];
+      const float sqi = __builtin_sqrtf(r.nrm[si]);
       int found = -1;
       if constexpr (D > 0) {
         float xi[D > 0 ? D : 4];
@@ -567,8 +587,8 @@ __global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ lis
           bool ok = false;
           if (j < i) {
             const uint32_t sj = s[j];
-            ok = cos_decide(dot_reg_mem<(D > 0 ? D : 4)>(xi, r.x + (size_t)sj * r.dp), ni,
-                            r.nrm[sj], thr);
+            ok = decide(dc, dot_reg_mem<(D > 0 ? D : 4)>(xi, r.x + (size_t)sj * r.dp),
+                        sqi * __builtin_sqrtf(r.nrm[sj]));
           }
           const uint64_t m = __ballot(ok);
           if (m) {
@@ -582,7 +602,8 @@ __global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ lis
           bool ok = false;
           if (j < i) {
             const uint32_t sj = s[j];
-            ok = cos_decide(dot_mem_mem(xip, r.x + (size_t)sj * r.dp, d), ni, r.nrm[sj], thr);
+            ok = decide(dc, dot_mem_mem(xip, r.x + (size_t)sj * r.dp, d),
+                        sqi * __builtin_sqrtf(r.nrm[sj]));
           }
           const uint64_t m = __ballot(ok);
           if (m) {
@@ -626,7 +647,7 @@ __global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ lis
 __global__ __launch_bounds__(256) void k_merge_lane_generic(const uint32_t* __restrict__ seg,
                                                             uint32_t hi, int bucket_thr,
                                                             uint32_t* __restrict__ slots,
-                                                            float thr, Rows r, MergeWork w,
+                                                            Decider dc, Rows r, MergeWork w,
                                                             Counters* ctr) {
   const uint32_t nseg = __hip_atomic_load(&ctr->n_seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int d = r.d;
@@ -645,11 +666,13 @@ __global__ __launch_bounds__(256) void k_merge_lane_generic(const uint32_t* __re
     while (i < size) {
       const uint32_t si = s[i];
       const float* xi = r.x + (size_t)si * r.dp;
-      const float ni = r.nrm[si];
+      const float sqi = __builtin_sqrtf(r.nrm[si]);
       uint32_t j = 0;
       for (; j < i; ++j) {
         const uint32_t sj = s[j];
-        if (cos_decide(dot_mem_mem(xi, r.x + (size_t)sj * r.dp, d), ni, r.nrm[sj], thr)) break;
+        if (decide(dc, dot_mem_mem(xi, r.x + (size_t)sj * r.dp, d),
+                   sqi * __builtin_sqrtf(r.nrm[sj])))
+          break;
       }
       if (j < i) {
         const uint32_t sj = s[j];
@@ -675,8 +698,46 @@ __global__ __launch_bounds__(256) void k_merge_lane_generic(const uint32_t* __re
 }
 
 // ----------------------------------------------------------------------------- launch -----
+// The smallest float s with fl(1 - fl(1 - s)) >= thr (cluster.cc:68-69), by bisection over the
+// ordered floats; see Decider.
+static float sim_roundtrip(float s) {
+  volatile float dist = 1.0f - s;
+  volatile float sim = 1.0f - dist;
+  return sim;
+}
+static uint32_t ordered(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+static float from_ordered(uint32_t o) {
+  const uint32_t u = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+Decider make_decider(float thr) {
+  Decider dc{std::numeric_limits<float>::quiet_NaN(), 0.0f, 0.0f, 0u};
+  uint32_t lo = ordered(-std::numeric_limits<float>::infinity());
+  uint32_t hi = ordered(std::numeric_limits<float>::infinity());
+  if (!(sim_roundtrip(from_ordered(hi)) >= thr)) return dc;  // nothing passes (thr NaN)
+  while (lo < hi) {  // invariant: hi passes
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (sim_roundtrip(from_ordered(mid)) >= thr) hi = mid;
+    else lo = mid + 1;
+  }
+  dc.s_star = from_ordered(hi);
+  if (dc.s_star >= 0x1p-60f && dc.s_star <= 0x1p60f) {
+    dc.s_lo = from_ordered(hi - 8);
+    dc.s_hi = from_ordered(hi + 8);
+    dc.fast = 1u;
+  }
+  return dc;
+}
+
 template <int D, int RB, int NT, bool ROWS_LDS>
-static void launch_big(const MergeWork& w, int c, uint32_t* slots, float thr, const Rows& r,
+static void launch_big(const MergeWork& w, int c, uint32_t* slots, const Decider& dc, const Rows& r,
                        Counters* ctr, uint32_t n, hipStream_t s) {
   using L = BigLayout<D, RB, ROWS_LDS>;
   static const bool lds_ok = [] {
@@ -687,46 +748,47 @@ static void launch_big(const MergeWork& w, int c, uint32_t* slots, float thr, co
   (void)lds_ok;
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
   const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
-  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, thr, r, ctr);
+  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr);
 }
 
 template <int D>
 static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
-                          uint32_t* slots, float thr, const MergeWork& w, Counters* ctr,
+                          uint32_t* slots, const Decider& dc, const MergeWork& w, Counters* ctr,
                           uint32_t n, hipStream_t s) {
   k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
   // Persistent grids: run counts live on the device; each grid strides over its list.
   auto grid = [&](int c, uint32_t per_wave) {
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
-  k_merge_group<2, D><<<grid(0, 32), 64, 0, s>>>(w.cls[0], 0, slots, thr, r, ctr);
-  k_merge_group<4, D><<<grid(1, 16), 64, 0, s>>>(w.cls[1], 1, slots, thr, r, ctr);
-  k_merge_group<8, D><<<grid(2, 8), 64, 0, s>>>(w.cls[2], 2, slots, thr, r, ctr);
-  k_merge_group<16, D><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, thr, r, ctr);
-  k_merge_group<32, D><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, thr, r, ctr);
-  k_merge_group<64, D><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, thr, r, ctr);
-  launch_big<D, 128, 128, true>(w, 0, slots, thr, r, ctr, n, s);
-  launch_big<D, 384, 256, true>(w, 1, slots, thr, r, ctr, n, s);
-  launch_big<D, 896, 256, false>(w, 2, slots, thr, r, ctr, n, s);
+  k_merge_group<2, D><<<grid(0, 32), 64, 0, s>>>(w.cls[0], 0, slots, dc, r, ctr);
+  k_merge_group<4, D><<<grid(1, 16), 64, 0, s>>>(w.cls[1], 1, slots, dc, r, ctr);
+  k_merge_group<8, D><<<grid(2, 8), 64, 0, s>>>(w.cls[2], 2, slots, dc, r, ctr);
+  k_merge_group<16, D><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, dc, r, ctr);
+  k_merge_group<32, D><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, dc, r, ctr);
+  k_merge_group<64, D><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, dc, r, ctr);
+  launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, s);
+  launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, s);
+  launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, s);
   const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 1] + 1) + 1);
-  k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, thr, r);
+  k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r);
 }
 
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
                   float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s) {
   if (hi <= lo) return;
   const uint32_t n = hi - lo;
+  const Decider dc = make_decider(thr);
   device_scan(SrcHead{key, lo}, DstSegStart{w.seg, lo}, n, w.tile_sums, &ctr->n_seg, s);
   switch (r.d) {
-    case 8: launch_groups<8>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
-    case 16: launch_groups<16>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
-    case 32: launch_groups<32>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
-    case 64: launch_groups<64>(r, w.seg, hi, bucket_thr, slots, thr, w, ctr, n, s); break;
+    case 8: launch_groups<8>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
+    case 16: launch_groups<16>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
+    case 32: launch_groups<32>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
+    case 64: launch_groups<64>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
     default: {
       const uint32_t g1 = (uint32_t)std::min<uint64_t>(4096, (n + 255) / 256);
-      k_merge_lane_generic<<<g1, 256, 0, s>>>(w.seg, hi, bucket_thr, slots, thr, r, w, ctr);
+      k_merge_lane_generic<<<g1, 256, 0, s>>>(w.seg, hi, bucket_thr, slots, dc, r, w, ctr);
       const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / 65 + 1);
-      k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, thr, r);
+      k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r);
     }
   }
 }

@@ -89,6 +89,35 @@ def test_pcluster_run_lengths_vs_oracle(engine, oracle, b, d, groups, noise, thr
     assert_same_result(engine.result(), *oracle.pcluster(rows, thr))
 
 
+def seq_sim(a, c):
+    """The reference's sim for one pair, op by op in fp32 (distance.cc:27-38)."""
+    f = np.float32
+    dot, na, nc = f(0), f(0), f(0)
+    for u, v in zip(a, c):
+        dot = f(dot + f(u * v))
+        na = f(na + f(u * u))
+        nc = f(nc + f(v * v))
+    return f(dot / f(np.sqrt(na) * np.sqrt(nc)))
+
+
+@pytest.mark.parametrize("b,d,step", [(40, 16, 0), (40, 16, 1), (40, 16, -1), (200, 64, 0),
+                                      (200, 64, 1), (600, 8, 0), (3000, 8, 0)])
+def test_pcluster_threshold_ties(engine, oracle, b, d, step):
+    """Thresholds exactly at (step 0) or one ulp either side of a pair's similarity: the merge
+    test's fast quotient bounds must hand these to the correctly rounded division."""
+    rng = np.random.default_rng(b + d)
+    rows = clustered(rng, b, d, max(2, b // 20), 0.08)
+    f = np.float32
+    for a, c in [(1, 0), (b // 2, b // 3), (b - 1, 2)]:
+        sim = seq_sim(rows[a], rows[c])
+        thr = f(f(1) - f(f(1) - sim))
+        for _ in range(abs(step)):
+            thr = np.nextafter(thr, f(np.inf if step > 0 else -np.inf), dtype=np.float32)
+        engine.load_rows(rows)
+        engine.pcluster(float(thr))
+        assert_same_result(engine.result(), *oracle.pcluster(rows, float(thr)))
+
+
 @pytest.mark.parametrize("b,d", [(33, 64), (1000, 16), (5000, 8)])
 def test_pcluster_identical_rows(engine, oracle, b, d):
     """Degenerate bucket (every row identical): the wave kernel merges i into j = 0 each step."""
