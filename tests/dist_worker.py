@@ -11,4 +11,6 @@ world, rank, local = bench.dist_setup()
 delay = 0.05 * (rank + 1)  # rank 1 is slower: the max must be rank 1's time
 elapsed, res = bench.timed(lambda: time.sleep(delay) or rank, steps=3, warmup=1, world=world,
                            local=local, sync=lambda _l: None)
-print(json.dumps({"rank": rank, "world": world, "elapsed": elapsed, "res": res}), flush=True)
+# one file per rank: two ranks printing to one pipe can interleave their lines
+with open(os.path.join(os.environ["KLSH_DIST_OUT"], f"rank{rank}.json"), "w") as f:
+    json.dump({"rank": rank, "world": world, "elapsed": elapsed, "res": res}, f)

@@ -17,13 +17,13 @@ def free_port():
     return p
 
 
-def test_two_rank_timing():
+def test_two_rank_timing(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "dist_worker.py")]
-    env = dict(os.environ, OMP_NUM_THREADS="1")
-    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300, env=env).stdout
-    recs = [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+    env = dict(os.environ, OMP_NUM_THREADS="1", KLSH_DIST_OUT=str(tmp_path))
+    subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300, env=env)
+    recs = [json.loads(p.read_text()) for p in sorted(tmp_path.glob("rank*.json"))]
     assert sorted(r["rank"] for r in recs) == [0, 1]
     e = {r["rank"]: r["elapsed"] for r in recs}
     assert e[0] == e[1]                 # max over ranks
