@@ -4,17 +4,19 @@ Metric (BASELINE.json): k-mers·iterations/s of the main Cluster() loop
 (reference app/kmerLSH.cc:490, function/cluster.cc:181-340) = N_0 * I / T_loop.
 
 Workload (BASELINE.json configs[1], "C2"): 10M k-mers x 64 samples, -I 500 -N 0.80.  Input is
-klsh-synth v1 (seed 11 + rank), converted on the GPU (mode C, convertHTMat) and
+klsh-synth v1 (seed 11), converted on the GPU (mode C, convertHTMat) and
 put through the reference's init pass (one iteration at 0.95, bucket threshold 1e5) before timing;
 the timed step is the main loop: restore the post-init state (device-to-device) and run all
 500 iterations (bucket threshold 1e6).  Inputs are resident in HBM when timing starts.
 
-Multi-GPU: one process per GPU (torch.distributed.run).  The loop does not shard without an
-exchange step; this round every rank clusters its own independent matrix
-(replicas, weak scaling, no data-path collective).  Barrier + max-over-ranks timing.
+Multi-GPU: one process per GPU (torch.distributed.run), BASELINE configs[2] ("C3"): the same
+10M x 64 problem sharded across the ranks by key range with RCCL exchanges over
+xGMI (keys/slots all-to-all, merge-delta allgather) and a result identical to 1 GPU: strong
+scaling, value = N_0 * I / T of the one job.  --mode replicas instead runs an independent matrix
+per rank (seed 11 + rank, no collective; weak scaling).  Barrier + max-over-ranks timing.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c4|c5]
-                    [--cpu-baseline auto|reference|port|none]
+                    [--mode sharded|replicas] [--cpu-baseline auto|reference|port|none]
 """
 from __future__ import annotations
 
@@ -56,7 +58,8 @@ def dist_setup():
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # timing scalars only: the data path has no collective (replicas)
+        # host-side control only (timing scalars, the RCCL id); the data path runs over RCCL
+        # inside the engine
         dist.init_process_group(backend="gloo", rank=rank, world_size=world)
     return world, rank, local
 
@@ -188,6 +191,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "none"])
+    ap.add_argument("--mode", default="sharded", choices=["sharded", "replicas"],
+                    help="N>1: one problem sharded over the ranks (C3) or one problem per rank")
     ap.add_argument("--iterations", type=int, default=0,
                     help="profiling only: override the config's -I (the metric is then not C2's)")
     args = ap.parse_args()
@@ -202,7 +207,15 @@ def main():
     from kmerlsh_amd import _native
 
     eng = _native.Engine(local)
-    counter0, kept, _ = prepare(eng, n0, d, seed=11 + rank)
+    sharded = world > 1 and args.mode == "sharded"
+    if sharded:
+        import torch.distributed as dist
+
+        uid = [_native.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(rank, world, uid[0])
+        log(f"rank {rank}/{world}: RCCL group up")
+    counter0, kept, _ = prepare(eng, n0, d, seed=11 if sharded else 11 + rank)
 
     def step():
         eng.restore()
@@ -214,9 +227,10 @@ def main():
 
     if rank != 0:
         return
-    value = world * n0 * iters * args.steps / elapsed
+    value = (1 if sharded else world) * n0 * iters * args.steps / elapsed
     agg = {k: sum(s[k] for s in stats) for k in stats[0]}
-    phases = {p: agg[p + "_ms"] / args.steps for p in ("project", "sort", "merge", "compact", "host")}
+    phases = {p: agg[p + "_ms"] / args.steps
+              for p in ("project", "sort", "merge", "compact", "host", "comm")}
     # dominant kernel: the projection (k_project<64>) unless another phase dominates
     launches = agg["project_launches"]
     proj_bytes = agg["sum_rows"] * (4 * d + 8)      # row read + slot read + key write
@@ -251,14 +265,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1000.0,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": f"synthetic klsh-synth v1 (seed 11+rank), {kept} rows kept of {n0}",
+        "data": (f"synthetic klsh-synth v1 (seed 11), {kept} rows kept of {n0}" if world == 1 or sharded
+                 else f"synthetic klsh-synth v1 (seed 11+rank), {kept} rows kept of {n0} per rank"),
         "config": {"workload": desc + " (main Cluster loop after the init pass)", "kmers": n0,
                    "samples": d, "iterations": iters, "min_similarity": min_sim,
                    "bucket_size_threshold": 1_000_000,
-                   "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+                   "parallelism": (f"sharded x{world} (key ranges, RCCL)" if sharded else
+                                   f"replicas x{world}" if world > 1 else "single GPU")},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "phases_ms_per_step": phases,

@@ -55,6 +55,8 @@ typedef struct klsh_stats {
   double merge_ms;         /* HIP-event time of the greedy in-bucket merge kernels */
   double compact_ms;       /* HIP-event time of the survivor compaction */
   double host_ms;          /* host-side hyperplane generation */
+  double comm_ms;          /* sharded loop: host time in inter-rank exchanges (incl. waits) */
+  uint64_t world;          /* ranks the call ran on (1 = single GPU) */
 } klsh_stats;
 
 /* ---- lifetime ------------------------------------------------------------------------------- */
@@ -92,6 +94,18 @@ int klsh_restore(klsh_ctx* ctx);
  * stats may be NULL. */
 int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket_size_threshold,
                  uint32_t seed_base, uint64_t* rng_counter, uint64_t* nt_trace, klsh_stats* stats);
+
+/* ---- multi-GPU: one rank per GPU, the loop sharded by key range -------------- */
+/* Every rank loads the same rows (replicas) and calls klsh_cluster with the same arguments; the
+ * result — order, rows, member lists and rng_counter — is identical to the single-GPU call on
+ * every rank.  RCCL (one process per GPU): rank 0 creates the 128-byte id, the caller ships it
+ * to the other ranks (any side channel), each rank calls klsh_comm_init on its context. */
+int klsh_comm_unique_id(uint8_t* id /* 128 bytes */);
+int klsh_comm_init(klsh_ctx* ctx, int rank, int world, const uint8_t* id /* 128 bytes */);
+/* In-process group over `world` contexts (any devices, several may share one GPU); each rank's
+ * klsh_cluster must then run on its own host thread, concurrently.  For tests on one GPU. */
+int klsh_comm_init_local(klsh_ctx** ctxs, int world);
+int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
 
 /* ---- results ---------------------------------------------------------------------------------- */
 int klsh_count(klsh_ctx* ctx, uint64_t* n_rows, uint64_t* n_members);

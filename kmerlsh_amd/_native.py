@@ -30,7 +30,8 @@ EXPORTED = (
     "klsh_create", "klsh_destroy", "klsh_last_error", "klsh_version", "klsh_load_rows",
     "klsh_load_counts", "klsh_snapshot", "klsh_restore", "klsh_cluster", "klsh_count",
     "klsh_result", "klsh_hash_keys", "klsh_pcluster", "klsh_hyperplanes", "klsh_fp_selftest",
-    "klsh_synth_counts",
+    "klsh_synth_counts", "klsh_comm_unique_id", "klsh_comm_init", "klsh_comm_init_local",
+    "klsh_comm_info",
 )
 
 
@@ -50,6 +51,8 @@ class KlshStats(ctypes.Structure):
         ("merge_ms", ctypes.c_double),
         ("compact_ms", ctypes.c_double),
         ("host_ms", ctypes.c_double),
+        ("comm_ms", ctypes.c_double),
+        ("world", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -99,6 +102,11 @@ def load_library() -> ctypes.CDLL:
         "klsh_fp_selftest": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P]),
         "klsh_synth_counts": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64,
                                              ctypes.c_uint64, ctypes.c_int, _P, _P]),
+        "klsh_comm_unique_id": (ctypes.c_int, [_P]),
+        "klsh_comm_init": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P]),
+        "klsh_comm_init_local": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
+        "klsh_comm_info": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -125,6 +133,21 @@ def hyperplanes(seed: int, counter: int, h: int, d: int) -> tuple[np.ndarray, in
     c = ctypes.c_uint64(counter)
     _check(lib.klsh_hyperplanes(seed, ctypes.byref(c), h, d, _ptr(out)), "klsh_hyperplanes")
     return out, c.value
+
+
+def comm_unique_id() -> bytes:
+    """128-byte RCCL id for klsh_comm_init (create on rank 0, ship to the others)."""
+    lib = load_library()
+    buf = (ctypes.c_uint8 * 128)()
+    _check(lib.klsh_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)), "klsh_comm_unique_id")
+    return bytes(buf)
+
+
+def comm_init_local(engines) -> None:
+    """Bind Engines into one in-process sharded group (each must then run on its own thread)."""
+    lib = load_library()
+    arr = (ctypes.c_void_p * len(engines))(*[e._ctx for e in engines])
+    _check(lib.klsh_comm_init_local(arr, len(engines)), "klsh_comm_init_local")
 
 
 def synth_counts(n: int, d: int, seed: int, genomes: int = 0, threads: int = 0):
@@ -187,6 +210,19 @@ class Engine:
         _check(self._lib.klsh_load_counts(self._ctx, _ptr(counts), n_total, batch_offset,
                                           batch_size, d, _ptr(vk)), "klsh_load_counts")
         self.d = d
+
+    def comm_init(self, rank: int, world: int, uid: bytes) -> None:
+        """Join the RCCL group `uid` as `rank` of `world` (one process per GPU)."""
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        _check(self._lib.klsh_comm_init(self._ctx, rank, world, ctypes.cast(buf, ctypes.c_void_p)),
+               "klsh_comm_init")
+
+    def comm_info(self) -> tuple[int, int]:
+        r = ctypes.c_int(0)
+        w = ctypes.c_int(1)
+        _check(self._lib.klsh_comm_info(self._ctx, ctypes.byref(r), ctypes.byref(w)),
+               "klsh_comm_info")
+        return r.value, w.value
 
     def snapshot(self) -> None:
         _check(self._lib.klsh_snapshot(self._ctx), "klsh_snapshot")

@@ -1,0 +1,54 @@
+// Inter-rank exchange for the sharded Cluster() loop (one rank = one klsh_ctx = one GPU).
+//
+// The loop needs four collective shapes per LSH iteration: an allgather of the
+// per-rank key-bin histograms, an all-to-all-v of (key, slot) pairs to the rank that owns each
+// key range, an allgather-v of merge deltas (rows rewritten by a merge), and small allgathers of
+// counters.  At the end of a call the member links are combined with an element-wise min.
+//
+// Two implementations behind one interface:
+//   RcclComm   one process per GPU, RCCL over xGMI (ncclSend/ncclRecv groups, ncclBroadcast,
+//              ncclAllGather, ncclAllReduce) — the product path, bench.py --gpus N.
+//   LocalComm  W contexts in ONE process, one host thread each (any devices, including W
+//              contexts on the same GPU): peer device-to-device copies behind host barriers.
+//              Lets the sharded path be tested bit-for-bit on a single GPU (RCCL refuses two
+//              ranks on one device).
+// All buffers are device pointers; every call is ordered on the caller's stream.  Sizes are in
+// bytes and must agree across ranks as each collective's contract says.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+
+namespace klsh {
+
+struct Comm {
+  int rank = 0;
+  int world = 1;
+  virtual ~Comm() {}
+  virtual const char* kind() const = 0;
+  // recv[r * bytes .. (r + 1) * bytes) = rank r's send[0 .. bytes).
+  virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // recv[offs[r] .. offs[r] + counts[r]) = rank r's send[0 .. counts[r]); counts/offs identical
+  // on every rank.
+  virtual int allgatherv(const void* send, void* recv, const size_t* counts, const size_t* offs,
+                         hipStream_t s) = 0;
+  // To rank r: send[soff[r] .. + scnt[r]); from rank r: recv[roff[r] .. + rcnt[r]).
+  virtual int alltoallv(const void* send, const size_t* scnt, const size_t* soff, void* recv,
+                        const size_t* rcnt, const size_t* roff, hipStream_t s) = 0;
+  // buf[i] = min over ranks of buf[i] (n uint32 elements), in place.
+  virtual int allreduce_min_u32(uint32_t* buf, size_t n, hipStream_t s) = 0;
+  std::string err;
+};
+
+// RCCL communicator on the calling thread's current device (one rank per process).
+Comm* make_rccl_comm(int rank, int world, const void* unique_id, int device, std::string* err);
+int rccl_unique_id(void* out128, std::string* err);
+
+// One in-process group of `world` ranks; returns the rank objects (owned by the caller).
+// Each rank's calls must come from its own host thread (they block on each other).
+void make_local_comms(int world, Comm** out);
+
+}  // namespace klsh

@@ -22,10 +22,12 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <numeric>
 #include <string>
 #include <vector>
 
 #include "klsh.h"
+#include "klsh_comm.h"
 #include "klsh_internal.h"
 
 extern "C" {
@@ -123,7 +125,67 @@ struct klsh_ctx {
   std::vector<uint64_t> ids;  // member node -> k-mer id
   Snapshot snap;
 
+  // sharded loop: this rank's exchange and its buffers (sized with the slots)
+  klsh::Comm* comm = nullptr;
+  uint2* sbuf = nullptr;       // (key, slot) pairs grouped by destination rank
+  uint2* rbuf = nullptr;       // (key, slot) pairs received, in source-rank order
+  uint32_t* cprev = nullptr;   // [slots] member counts before this iteration's merge
+  uint32_t* dslots = nullptr;  // survivors rewritten by a merge (this rank)
+  uint32_t* bins = nullptr;    // [4096] key-bin histogram of this rank
+  uint32_t* bins_all = nullptr;
+  uint32_t* owner = nullptr;   // [4096] bin -> rank
+  uint32_t* cntmat = nullptr;  // [W][W] pairs rank g sends rank r
+  uint32_t* small = nullptr;   // [W + 1][4] per-rank counters exchange
+  uint32_t* h_small = nullptr; // pinned: cntmat or the counters exchange
+  uint32_t* drec = nullptr;    // delta records of this rank, then of all ranks
+  uint32_t* drec_all = nullptr;
+  size_t drec_cap = 0, drec_all_cap = 0;  // words
+  uint64_t shard_cap = 0;
+
   ~klsh_ctx() { release(); }
+
+  int world() const { return comm ? comm->world : 1; }
+  int rank() const { return comm ? comm->rank : 0; }
+
+  void release_shard() {
+    dfree(sbuf); dfree(rbuf); dfree(cprev); dfree(dslots); dfree(bins); dfree(bins_all);
+    dfree(owner); dfree(cntmat); dfree(small); dfree(drec); dfree(drec_all);
+    if (h_small) (void)hipHostFree(h_small);
+    h_small = nullptr;
+    drec_cap = drec_all_cap = 0;
+    shard_cap = 0;
+  }
+  int reserve_shard() {
+    const int W = world();
+    if (shard_cap >= cap_slots && sbuf) return 0;
+    release_shard();
+    const uint64_t s = std::max<uint64_t>(cap_slots, 1);
+    const size_t nb = (size_t)1 << klsh::kMaxBinBits;
+    int e = 0;
+    if ((e = dalloc(&sbuf, s)) || (e = dalloc(&rbuf, s)) || (e = dalloc(&cprev, s)) ||
+        (e = dalloc(&dslots, s)) || (e = dalloc(&bins, nb)) || (e = dalloc(&bins_all, nb * W)) ||
+        (e = dalloc(&owner, nb)) || (e = dalloc(&cntmat, (size_t)W * W)) ||
+        (e = dalloc(&small, (size_t)(W + 1) * 4))) {
+      release_shard();
+      return e;
+    }
+    if (hipHostMalloc((void**)&h_small, sizeof(uint32_t) * std::max(W * W, (W + 1) * 4),
+                      hipHostMallocDefault) != hipSuccess) {
+      release_shard();
+      return fail(KLSH_E_NOMEM, "pinned exchange buffer");
+    }
+    shard_cap = s;
+    return 0;
+  }
+  int reserve_words(uint32_t** p, size_t* cap, size_t words) {
+    if (words <= *cap && *p) return 0;
+    dfree(*p);
+    *cap = 0;
+    const size_t w = std::max<size_t>(words + words / 4, 1 << 16);
+    if (int e = dalloc(p, w)) return e;
+    *cap = w;
+    return 0;
+  }
 
   void release_state() {
     dfree(rows.x); dfree(rows.nrm); dfree(rows.cnt); dfree(rows.head); dfree(rows.tail);
@@ -142,6 +204,9 @@ struct klsh_ctx {
     snap.valid = false;
   }
   void release() {
+    release_shard();
+    delete comm;
+    comm = nullptr;
     release_state();
     dfree(W);
     dfree(ctr);
@@ -458,14 +523,13 @@ int klsh_restore(klsh_ctx* ctx) {
   return 0;
 }
 
-// Merge + compaction of one iteration's sorted runs, plus the nested path for oversize buckets.
-// fk/fv: sorted keys/slots (fv is one of ctx->order / ctx->alt).  Returns with the new canonical
-// order in ctx->order and ctx->n_live updated.
-static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
-                             int bucket_thr, uint32_t seed_base, uint64_t* rng_counter,
-                             klsh_stats* st, bool timed) {
+// Merge + compaction of one iteration's sorted runs (fk/fv, n positions, in place on fv) into
+// `out`; with `prev` (sharded loop) also the list of survivors a merge rewrote (merge deltas).
+// Ends with the counters on the host: total (survivors), n_over (oversize runs), n_delta.
+static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
+                      int bucket_thr, uint32_t* out, const uint32_t* prev, klsh_stats* st,
+                      bool timed) {
   hipStream_t s = ctx->stream;
-  uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
   klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->mw, ctx->ctr, s);
   KLSH_HIP(hipGetLastError());
@@ -473,49 +537,309 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
   klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
+  if (prev) {
+    klsh::launch_delta_select(out, n, ctx->rows.cnt, prev, ctx->dslots, ctx->tile_sums, ctx->ctr, s);
+    KLSH_HIP(hipGetLastError());
+  }
   if (int e = ctx->sync_counters()) return e;
   if (timed && st) {
     st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
     st->compact_ms += elapsed(ctx->ev[3], ctx->ev[4]);
   }
+  return 0;
+}
+
+// The oversize runs of the last merge_main, ascending (the reference's T=1 order):
+// (start, length) pairs and the hyperplanes their nestedCluster calls draw (floor(log2 b) each).
+static int oversize_runs(klsh_ctx* ctx, std::vector<uint2>* over, uint64_t* hyperplanes) {
   const uint32_t n_over = ctx->h_ctr->n_over;
-  if (n_over > 0) {
-    // nestedCluster (cluster.cc:286-288 -> :89-178) for each oversize bucket, ascending.
-    std::vector<uint2> over(n_over);
-    KLSH_HIP(hipMemcpy(over.data(), ctx->mw.over, sizeof(uint2) * n_over, hipMemcpyDeviceToHost));
-    std::sort(over.begin(), over.end(), [](const uint2& a, const uint2& b) { return a.x < b.x; });
-    for (uint32_t oi = 0; oi < n_over; ++oi) {
-      const uint32_t p = over[oi].x, b = over[oi].y;
-      const int h2 = floor_log2(b);
-      const uint64_t k = *rng_counter;
-      *rng_counter += (uint64_t)h2;
-      if (st) {
-        st->hyperplanes += (uint64_t)h2;
-        st->nested_calls += 1;
-      }
-      if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h2, st ? &st->host_ms : nullptr))
-        return e;
-      // Sub-keys carry bit 31 (main keys are < 2^h <= 2^31, so never have it) and a bit 30 that
-      // alternates between consecutive oversize regions, so no run crosses a region boundary.
-      const uint32_t key_or = 0x80000000u | ((oi & 1u) << 30);
-      klsh::launch_project(ctx->rows, fv + p, ctx->nk1, b, ctx->hyperplane_ptr(k), h2, key_or, s);
-      uint32_t *rk = nullptr, *rv = nullptr;
-      klsh::radix_sort(ctx->nk1, fv + p, ctx->nk2, ctx->nv2, b, h2, ctx->hist, ctx->tile_sums,
-                       ctx->ctr, &rk, &rv, s);
-      KLSH_HIP(hipMemcpyAsync(fk + p, rk, 4ull * b, hipMemcpyDeviceToDevice, s));
-      if (rv != fv + p) KLSH_HIP(hipMemcpyAsync(fv + p, rv, 4ull * b, hipMemcpyDeviceToDevice, s));
-      // fresh run lists for the region (n_seg .. n_over are contiguous)
-      KLSH_HIP(hipMemsetAsync(&ctx->ctr->n_seg, 0,
-                              offsetof(Counters, total) - offsetof(Counters, n_seg), s));
-      klsh::launch_merge(ctx->rows, fk, fv, p, p + b, thr, -1, ctx->mw, ctx->ctr, s);
-      KLSH_HIP(hipGetLastError());
+  over->resize(n_over);
+  *hyperplanes = 0;
+  if (n_over == 0) return 0;
+  KLSH_HIP(hipMemcpy(over->data(), ctx->mw.over, sizeof(uint2) * n_over, hipMemcpyDeviceToHost));
+  std::sort(over->begin(), over->end(), [](const uint2& a, const uint2& b) { return a.x < b.x; });
+  for (const uint2& o : *over) *hyperplanes += (uint64_t)floor_log2(o.y);
+  return 0;
+}
+
+// nestedCluster (cluster.cc:286-288 -> :89-178) for each oversize run, ascending, drawing
+// hyperplanes from *rng_counter on; then the survivors are compacted again into `out` (and the
+// delta list rebuilt with `prev`).  Ends with the counters on the host.
+static int merge_nested(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
+                        const std::vector<uint2>& over, uint32_t seed_base, uint64_t* rng_counter,
+                        uint32_t* out, const uint32_t* prev, klsh_stats* st) {
+  hipStream_t s = ctx->stream;
+  for (uint32_t oi = 0; oi < (uint32_t)over.size(); ++oi) {
+    const uint32_t p = over[oi].x, b = over[oi].y;
+    const int h2 = floor_log2(b);
+    const uint64_t k = *rng_counter;
+    *rng_counter += (uint64_t)h2;
+    if (st) {
+      st->hyperplanes += (uint64_t)h2;
+      st->nested_calls += 1;
     }
-    klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
+    if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h2, st ? &st->host_ms : nullptr))
+      return e;
+    // Sub-keys carry bit 31 (main keys are < 2^h <= 2^31, so never have it) and a bit 30 that
+    // alternates between consecutive oversize regions, so no run crosses a region boundary.
+    const uint32_t key_or = 0x80000000u | ((oi & 1u) << 30);
+    klsh::launch_project(ctx->rows, fv + p, ctx->nk1, b, ctx->hyperplane_ptr(k), h2, key_or, s);
+    uint32_t *rk = nullptr, *rv = nullptr;
+    klsh::radix_sort(ctx->nk1, fv + p, ctx->nk2, ctx->nv2, b, h2, ctx->hist, ctx->tile_sums,
+                     ctx->ctr, &rk, &rv, s);
+    KLSH_HIP(hipMemcpyAsync(fk + p, rk, 4ull * b, hipMemcpyDeviceToDevice, s));
+    if (rv != fv + p) KLSH_HIP(hipMemcpyAsync(fv + p, rv, 4ull * b, hipMemcpyDeviceToDevice, s));
+    // fresh run lists for the region (n_seg .. n_over are contiguous)
+    KLSH_HIP(hipMemsetAsync(&ctx->ctr->n_seg, 0,
+                            offsetof(Counters, total) - offsetof(Counters, n_seg), s));
+    klsh::launch_merge(ctx->rows, fk, fv, p, p + b, thr, -1, ctx->mw, ctx->ctr, s);
     KLSH_HIP(hipGetLastError());
-    if (int e = ctx->sync_counters()) return e;
+  }
+  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
+  KLSH_HIP(hipGetLastError());
+  if (prev) {
+    klsh::launch_delta_select(out, n, ctx->rows.cnt, prev, ctx->dslots, ctx->tile_sums, ctx->ctr, s);
+    KLSH_HIP(hipGetLastError());
+  }
+  return ctx->sync_counters();
+}
+
+// Single-GPU: merge, compaction and nested buckets of one iteration.  fk/fv: sorted keys/slots
+// (fv is one of ctx->order / ctx->alt).  Returns with the new canonical order in ctx->order and
+// ctx->n_live updated.
+static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
+                             int bucket_thr, uint32_t seed_base, uint64_t* rng_counter,
+                             klsh_stats* st, bool timed) {
+  uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
+  if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, nullptr, st, timed)) return e;
+  if (ctx->h_ctr->n_over > 0) {
+    std::vector<uint2> over;
+    uint64_t hyp = 0;
+    if (int e = oversize_runs(ctx, &over, &hyp)) return e;
+    if (int e = merge_nested(ctx, fk, fv, n, thr, over, seed_base, rng_counter, out, nullptr, st))
+      return e;
   }
   if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
   ctx->n_live = ctx->h_ctr->total;
+  return 0;
+}
+
+// ============================================================ sharded loop ===
+// Every rank holds a replica of the rows; the canonical order of iteration t is the concatenation
+// over ranks of each rank's survivors ("mine").  Per iteration:
+//   project mine -> keys; bin histogram (top <= 12 key bits) -> allgather -> every rank derives
+//   the same bin -> rank ownership (contiguous key ranges balanced by rows) and send counts;
+//   stable partition of (key, slot) by owner -> all-to-all-v -> received pairs are in canonical
+//   order restricted to this rank's key range; stable radix sort by key = merge_hashtable's
+//   bucket order for those keys; greedy merge + compaction -> the new "mine"; the survivors a
+//   merge rewrote are broadcast (allgather-v of rows + metadata) so every replica stays identical.
+// Oversize buckets (nestedCluster) draw hyperplanes in ascending bucket order, i.e. rank order
+// then local order: a small allgather of (runs, hyperplanes) gives each rank its RNG offset.
+// Member links are written only by the rank that merged them; the end of the call combines them
+// with an element-wise min (an unwritten link is kNil = 0xFFFFFFFF) and gathers the global order.
+static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
+                           int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
+                           uint64_t* nt_trace, klsh_stats* st) {
+  klsh::Comm* cm = ctx->comm;
+  const int W = cm->world, g = cm->rank;
+  hipStream_t s = ctx->stream;
+  if (int e = ctx->reserve_shard()) return e;
+  auto comm_fail = [&](const char* what) {
+    return fail(KLSH_E_HIP, std::string(what) + ": " + cm->err);
+  };
+  const double t_start = now_ms();
+  double t_comm = 0.0;
+  auto timed_comm = [&](auto fn) {
+    const double t0 = now_ms();
+    const int rc = fn();
+    t_comm += now_ms() - t0;
+    return rc;
+  };
+
+  const float max_similarity = 0.95f;  // cluster.cc:190-192 (all float)
+  const float sim_step = (max_similarity - min_similarity) / (float)iterations;
+  float threshold = max_similarity;
+
+  // my block of the global canonical order
+  uint64_t N = ctx->n_live;
+  uint32_t n_g = 0;
+  {
+    const uint64_t lo = N * (uint64_t)g / (uint64_t)W, hi = N * (uint64_t)(g + 1) / (uint64_t)W;
+    n_g = (uint32_t)(hi - lo);
+    if (n_g) KLSH_HIP(hipMemcpyAsync(ctx->alt, ctx->order + lo, 4ull * n_g, hipMemcpyDeviceToDevice, s));
+    std::swap(ctx->order, ctx->alt);
+  }
+  std::vector<uint32_t> n_all(W, 0);  // survivors per rank after the last exchange
+  for (int r = 0; r < W; ++r)
+    n_all[r] = (uint32_t)(N * (uint64_t)(r + 1) / W - N * (uint64_t)r / W);
+
+  ctx->w_count = 0;
+  if (N > 0 && iterations > 0) {
+    const uint64_t hmax = (uint64_t)floor_log2(N);
+    if (int e = ctx->ensure_hyperplanes(seed_base, *rng_counter, hmax * (uint64_t)iterations,
+                                        &st->host_ms))
+      return e;
+  }
+  const int R = klsh::delta_words(ctx->dp);
+  std::vector<size_t> scnt(W), soff(W), rcnt(W), roff(W), dcnt(W), doff(W);
+
+  for (int it = 0; it < iterations; ++it) {
+    if (nt_trace) nt_trace[it] = N;
+    st->iterations += 1;
+    if (N == 0) {
+      threshold -= sim_step;
+      continue;
+    }
+    const int h = floor_log2(N);
+    const uint64_t k = *rng_counter;
+    *rng_counter += (uint64_t)h;
+    st->hyperplanes += (uint64_t)h;
+    if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h, &st->host_ms)) return e;
+
+    // 1. keys of my rows, key-range ownership, send counts
+    KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    KLSH_HIP(hipEventRecord(ctx->ev[0], s));
+    klsh::launch_project(ctx->rows, ctx->order, ctx->keys, n_g, ctx->hyperplane_ptr(k), h, 0u, s);
+    KLSH_HIP(hipGetLastError());
+    KLSH_HIP(hipEventRecord(ctx->ev[1], s));
+    const int B = std::min(h, klsh::kMaxBinBits);
+    const int shift = h - B;
+    const uint32_t nbins = 1u << B;
+    klsh::launch_bin_hist(ctx->keys, n_g, shift, nbins, ctx->bins, s);
+    if (timed_comm([&] { return cm->allgather(ctx->bins, ctx->bins_all, 4ull * nbins, s); }))
+      return comm_fail("bin histogram allgather");
+    klsh::launch_bin_split(ctx->bins_all, W, nbins, N, ctx->owner, ctx->cntmat, s);
+    KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->cntmat, 4ull * W * W, hipMemcpyDeviceToHost, s));
+    KLSH_HIP(hipStreamSynchronize(s));
+    uint32_t m_g = 0;
+    for (int r = 0; r < W; ++r) {
+      scnt[r] = 8ull * ctx->h_small[g * W + r];
+      rcnt[r] = 8ull * ctx->h_small[r * W + g];
+      soff[r] = r ? soff[r - 1] + scnt[r - 1] : 0;
+      roff[r] = r ? roff[r - 1] + rcnt[r - 1] : 0;
+      m_g += ctx->h_small[r * W + g];
+    }
+
+    // 2. exchange (key, slot) pairs: stable partition by owner, all-to-all-v
+    uint32_t *dk = nullptr, *dv = nullptr;
+    klsh::launch_dest(ctx->keys, n_g, shift, ctx->owner, ctx->nk1, ctx->nk2, s);
+    klsh::radix_sort(ctx->nk1, ctx->nk2, ctx->nv2, ctx->keys2, n_g, 8, ctx->hist, ctx->tile_sums,
+                     ctx->ctr, &dk, &dv, s);
+    klsh::launch_pack_pairs(ctx->keys, ctx->order, dv, n_g, ctx->sbuf, s);
+    KLSH_HIP(hipGetLastError());
+    if (timed_comm([&] {
+          return cm->alltoallv(ctx->sbuf, scnt.data(), soff.data(), ctx->rbuf, rcnt.data(),
+                               roff.data(), s);
+        }))
+      return comm_fail("pair all-to-all");
+    klsh::launch_unpack_pairs(ctx->rbuf, m_g, ctx->keys, ctx->alt, ctx->rows.cnt, ctx->cprev, s);
+    KLSH_HIP(hipEventRecord(ctx->ev[6], s));
+
+    // 3. bucket order of my key range, merge, compaction, delta list
+    uint32_t *fk = nullptr, *fv = nullptr;
+    klsh::radix_sort(ctx->keys, ctx->alt, ctx->keys2, ctx->order, m_g, h, ctx->hist,
+                     ctx->tile_sums, ctx->ctr, &fk, &fv, s);
+    KLSH_HIP(hipGetLastError());
+    KLSH_HIP(hipEventRecord(ctx->ev[5], s));
+    uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
+    if (int e = merge_main(ctx, fk, fv, m_g, threshold, bucket_size_threshold, out, ctx->cprev, st,
+                           true))
+      return e;
+    std::vector<uint2> over;
+    uint64_t my_hyp = 0;
+    if (int e = oversize_runs(ctx, &over, &my_hyp)) return e;
+
+    // 4. counters of every rank: survivors, deltas, oversize runs and their hyperplanes
+    auto exchange_counters = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) -> int {
+      uint32_t* hs = ctx->h_small;
+      hs[0] = a; hs[1] = b; hs[2] = c; hs[3] = d;
+      KLSH_HIP(hipMemcpyAsync(ctx->small + 4 * W, hs, 16, hipMemcpyHostToDevice, s));
+      if (timed_comm([&] { return cm->allgather(ctx->small + 4 * W, ctx->small, 16, s); }))
+        return comm_fail("counter allgather");
+      KLSH_HIP(hipMemcpyAsync(hs, ctx->small, 16ull * W, hipMemcpyDeviceToHost, s));
+      KLSH_HIP(hipStreamSynchronize(s));
+      return 0;
+    };
+    if (int e = exchange_counters(ctx->h_ctr->total, ctx->h_ctr->n_delta, (uint32_t)over.size(),
+                                  (uint32_t)my_hyp))
+      return e;
+    std::vector<uint32_t> surv(W), ndel(W);
+    uint64_t any_over = 0, hyp_before = 0, hyp_all = 0;
+    for (int r = 0; r < W; ++r) {
+      surv[r] = ctx->h_small[4 * r];
+      ndel[r] = ctx->h_small[4 * r + 1];
+      any_over += ctx->h_small[4 * r + 2];
+      if (r < g) hyp_before += ctx->h_small[4 * r + 3];
+      hyp_all += ctx->h_small[4 * r + 3];
+    }
+    if (any_over) {
+      uint64_t rng = *rng_counter + hyp_before;
+      if (!over.empty()) {
+        if (int e = merge_nested(ctx, fk, fv, m_g, threshold, over, seed_base, &rng, out,
+                                 ctx->cprev, st))
+          return e;
+      }
+      *rng_counter += hyp_all;
+      if (int e = exchange_counters(ctx->h_ctr->total, ctx->h_ctr->n_delta, 0, 0)) return e;
+      for (int r = 0; r < W; ++r) {
+        surv[r] = ctx->h_small[4 * r];
+        ndel[r] = ctx->h_small[4 * r + 1];
+      }
+    }
+
+    // 5. merge deltas to every replica
+    uint64_t nd_all = 0;
+    for (int r = 0; r < W; ++r) {
+      dcnt[r] = 4ull * R * ndel[r];
+      doff[r] = 4ull * R * nd_all;
+      nd_all += ndel[r];
+    }
+    if (nd_all) {
+      if (int e = ctx->reserve_words(&ctx->drec, &ctx->drec_cap, (size_t)R * ndel[g] + 1)) return e;
+      if (int e = ctx->reserve_words(&ctx->drec_all, &ctx->drec_all_cap, (size_t)R * nd_all)) return e;
+      klsh::launch_delta_pack(ctx->rows, ctx->dslots, ndel[g], ctx->drec, s);
+      if (timed_comm([&] {
+            return cm->allgatherv(ctx->drec, ctx->drec_all, dcnt.data(), doff.data(), s);
+          }))
+        return comm_fail("delta allgather");
+      klsh::launch_delta_apply(ctx->rows, ctx->drec_all, (uint32_t)nd_all, s);
+      KLSH_HIP(hipGetLastError());
+    }
+
+    if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
+    const uint64_t N_next = std::accumulate(surv.begin(), surv.end(), (uint64_t)0);
+    st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
+    st->sort_ms += elapsed(ctx->ev[6], ctx->ev[5]);
+    st->project_launches += 1;
+    st->sum_rows += N;
+    st->sum_proj_bits += N * (uint64_t)h;
+    st->sum_merges += N - N_next;
+    N = N_next;
+    n_g = surv[g];
+    n_all = surv;
+    threshold -= sim_step;
+  }
+
+  // global canonical order on every rank, combined member links
+  {
+    std::vector<size_t> cnt(W), off(W);
+    size_t acc = 0;
+    for (int r = 0; r < W; ++r) {
+      cnt[r] = 4ull * n_all[r];
+      off[r] = acc;
+      acc += cnt[r];
+    }
+    if (timed_comm([&] { return cm->allgatherv(ctx->order, ctx->alt, cnt.data(), off.data(), s); }))
+      return comm_fail("order allgather");
+    std::swap(ctx->order, ctx->alt);
+    if (timed_comm([&] { return cm->allreduce_min_u32(ctx->rows.nxt, ctx->members, s); }))
+      return comm_fail("member link allreduce");
+    KLSH_HIP(hipStreamSynchronize(s));
+  }
+  ctx->n_live = N;
+  st->n_final = N;
+  st->comm_ms = t_comm;
+  st->wall_ms = now_ms() - t_start;
   return 0;
 }
 
@@ -527,6 +851,10 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   klsh_stats local{};
   klsh_stats* st = stats ? stats : &local;
   memset(st, 0, sizeof(*st));
+  st->world = (uint64_t)ctx->world();
+  if (ctx->world() > 1)
+    return cluster_sharded(ctx, min_similarity, iterations, bucket_size_threshold, seed_base,
+                           rng_counter, nt_trace, st);
   const double t_start = now_ms();
   hipStream_t s = ctx->stream;
 
@@ -612,6 +940,47 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   }
   st->n_final = ctx->n_live;
   st->wall_ms = now_ms() - t_start;
+  return 0;
+}
+
+int klsh_comm_unique_id(uint8_t* id) {
+  if (!id) return fail(KLSH_E_ARG, "null argument");
+  std::string err;
+  if (klsh::rccl_unique_id(id, &err)) return fail(KLSH_E_HIP, err);
+  return 0;
+}
+
+int klsh_comm_init(klsh_ctx* ctx, int rank, int world, const uint8_t* id) {
+  if (!ctx || !id || world < 1 || rank < 0 || rank >= world || world > klsh::kMaxRanks)
+    return fail(KLSH_E_ARG, "bad argument");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  std::string err;
+  klsh::Comm* c = klsh::make_rccl_comm(rank, world, id, ctx->device, &err);
+  if (!c) return fail(KLSH_E_HIP, err);
+  ctx->release_shard();
+  delete ctx->comm;
+  ctx->comm = c;
+  return 0;
+}
+
+int klsh_comm_init_local(klsh_ctx** ctxs, int world) {
+  if (!ctxs || world < 1 || world > klsh::kMaxRanks) return fail(KLSH_E_ARG, "bad argument");
+  for (int r = 0; r < world; ++r)
+    if (!ctxs[r]) return fail(KLSH_E_ARG, "null context");
+  std::vector<klsh::Comm*> cs(world);
+  klsh::make_local_comms(world, cs.data());
+  for (int r = 0; r < world; ++r) {
+    ctxs[r]->release_shard();
+    delete ctxs[r]->comm;
+    ctxs[r]->comm = cs[r];
+  }
+  return 0;
+}
+
+int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world) {
+  if (!ctx) return fail(KLSH_E_ARG, "null ctx");
+  if (rank) *rank = ctx->rank();
+  if (world) *world = ctx->world();
   return 0;
 }
 

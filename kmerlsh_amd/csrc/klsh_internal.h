@@ -32,7 +32,8 @@ struct Counters {
   uint32_t n_huge;                 // longer runs queued for k_merge_wave
   uint32_t n_over;                 // runs longer than bucket_size_threshold (nestedCluster)
   uint32_t total;                  // result of the last scan/compaction (live rows)
-  uint32_t pad[3];
+  uint32_t n_delta;                // sharded loop: survivors rewritten by a merge this iteration
+  uint32_t pad[2];
 };
 
 // Merge workspace (device), sized for `cap` positions.
@@ -109,5 +110,38 @@ void launch_gather_rows(const Rows& r, const uint32_t* order, uint32_t n, float*
 // kernels evaluate them.
 void launch_fp_selftest(const float* a, const float* b, uint32_t n, float* sqrt_out,
                         float* div_out, hipStream_t s);
+
+// ---- sharded loop (klsh_shard.hip) ----------------------------------------------
+constexpr int kMaxBinBits = 12;           // key ranges are unions of 2^12 top-bit bins
+constexpr int kMaxRanks = 64;
+
+// hist[bin] += 1 for every key (bin = key >> shift, < nbins); hist zeroed by the caller.
+void launch_bin_hist(const uint32_t* keys, uint32_t n, int shift, uint32_t nbins, uint32_t* hist,
+                     hipStream_t s);
+// From every rank's histogram (hist_all[W][nbins]) and the total row count: owner[bin] = the rank
+// owning the bin (contiguous, balanced by rows), cntmat[g * W + r] = rows rank g sends rank r.
+void launch_bin_split(const uint32_t* hist_all, int world, uint32_t nbins, uint64_t total,
+                      uint32_t* owner, uint32_t* cntmat, hipStream_t s);
+// dest[i] = owner[keys[i] >> shift]; idx[i] = i.
+void launch_dest(const uint32_t* keys, uint32_t n, int shift, const uint32_t* owner,
+                 uint32_t* dest, uint32_t* idx, hipStream_t s);
+// out[i] = (keys[idx[i]], slots[idx[i]]).
+void launch_pack_pairs(const uint32_t* keys, const uint32_t* slots, const uint32_t* idx,
+                       uint32_t n, uint2* out, hipStream_t s);
+// keys[i] = in[i].x, slots[i] = in[i].y; prev[slots[i]] = cnt[slots[i]] (member counts before
+// the merge: a survivor whose count changed was rewritten).
+void launch_unpack_pairs(const uint2* in, uint32_t n, uint32_t* keys, uint32_t* slots,
+                         const uint32_t* cnt, uint32_t* prev, hipStream_t s);
+// delta_slots[0..ctr->n_delta) = survivors s (in order) with cnt[s] != prev[s].
+void launch_delta_select(const uint32_t* surv, uint32_t n, const uint32_t* cnt,
+                         const uint32_t* prev, uint32_t* delta_slots, uint32_t* tile_sums,
+                         Counters* ctr, hipStream_t s);
+// Delta records, stride 5 + dp words: slot, cnt, head, tail, nrm bits, row[dp].
+__host__ __device__ inline int delta_words(int dp) { return 5 + dp; }
+void launch_delta_pack(const Rows& r, const uint32_t* delta_slots, uint32_t n, uint32_t* rec,
+                       hipStream_t s);
+void launch_delta_apply(const Rows& r, const uint32_t* rec, uint32_t n, hipStream_t s);
+// a[i] = min(a[i], b[i])
+void launch_min_u32(uint32_t* a, const uint32_t* b, size_t n, hipStream_t s);
 
 }  // namespace klsh

@@ -17,6 +17,9 @@
 
 #include <stdlib.h>
 
+#include <string>
+#include <type_traits>
+
 #include "klsh_device.cuh"
 
 namespace klsh {
@@ -74,6 +77,98 @@ __global__ __launch_bounds__(256) void k_project(const float* __restrict__ X, in
   keys[p] = key | key_or;
 }
 
+// Packed-f32 projection.  The same sequential chains as k_project, two per instruction:
+// v_pk_mul_f32 / v_pk_add_f32 round each half exactly like v_mul_f32 / v_add_f32 (no fusion,
+// -ffp-contract=off), so the keys are bit-identical, at twice the f32 VALU issue rate — the
+// unpacked kernel sits at the non-packed VALU ceiling (2·h·d single-rate ops per row), not at HBM.
+// Hyperplanes sit in LDS as [h/4][D] float4 quads (w_4q[k], w_4q+1[k], w_4q+2[k], w_4q+3[k]), so
+// one broadcast ds_read_b128 feeds 4 chains at column k; h is padded to a multiple of 4 with
+// zero hyperplanes whose bits are dropped.  CH quads (4·CH chains) run at once for ILP.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+#ifndef KLSH_PK_WAVES
+#define KLSH_PK_WAVES 4
+#endif
+
+
+// acc + w * (x, x), x one half of a register pair (op_sel picks the half; no register copies).
+// Multiply and add stay one asm block so the scheduler cannot hoist the products of every
+// column ahead of the chain (that spilled); both are separately rounded, never fused.
+__device__ __forceinline__ void pk_mac_lo(f32x2& acc, f32x2 w, f32x2 x) {
+  f32x2 t;
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[1,0]\n\tv_pk_add_f32 %0, %0, %1"
+      : "+v"(acc), "=&v"(t) : "v"(w), "v"(x));
+}
+__device__ __forceinline__ void pk_mac_hi(f32x2& acc, f32x2 w, f32x2 x) {
+  f32x2 t;
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel:[0,1] op_sel_hi:[1,1]\n\tv_pk_add_f32 %0, %0, %1"
+      : "+v"(acc), "=&v"(t) : "v"(w), "v"(x));
+}
+
+template <int D, int CH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KLSH_PK_WAVES)))
+void k_project_pk(const float* __restrict__ X, int dp,
+                                                    const uint32_t* __restrict__ slots,
+                                                    uint32_t* __restrict__ keys, uint32_t n,
+                                                    const float* __restrict__ W, int h,
+                                                    uint32_t key_or) {
+  constexpr int QMAX = kMaxHyperplanes / 4;
+  __shared__ __attribute__((aligned(16))) float4 sw[QMAX * D];
+  const int nq = (h + 3) >> 2;
+  for (int i = threadIdx.x; i < nq * D; i += 256) {
+    const int q = i / D, k = i % D;
+    float4 v;
+    v.x = 4 * q + 0 < h ? W[(4 * q + 0) * dp + k] : 0.0f;
+    v.y = 4 * q + 1 < h ? W[(4 * q + 1) * dp + k] : 0.0f;
+    v.z = 4 * q + 2 < h ? W[(4 * q + 2) * dp + k] : 0.0f;
+    v.w = 4 * q + 3 < h ? W[(4 * q + 3) * dp + k] : 0.0f;
+    sw[i] = v;
+  }
+  const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+  __syncthreads();
+  if (p >= n) return;
+  f32x2 x[D / 2];  // (x[2m], x[2m+1])
+  {
+    const float4* src = reinterpret_cast<const float4*>(X + (size_t)slots[p] * dp);
+#pragma unroll
+    for (int m = 0; m < D / 4; ++m) {
+      const float4 v = src[m];
+      x[2 * m] = (f32x2){v.x, v.y};
+      x[2 * m + 1] = (f32x2){v.z, v.w};
+    }
+  }
+  uint32_t key = 0;
+  auto quads = [&](int q, auto ch) {
+    constexpr int C = decltype(ch)::value;
+    f32x2 a[C][2];
+#pragma unroll
+    for (int c = 0; c < C; ++c) a[c][0] = a[c][1] = (f32x2){0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float4 w = sw[(q + c) * D + k];
+        const f32x2 w01 = (f32x2){w.x, w.y}, w23 = (f32x2){w.z, w.w};
+        if (k & 1) {
+          pk_mac_hi(a[c][0], w01, x[k / 2]);
+          pk_mac_hi(a[c][1], w23, x[k / 2]);
+        } else {
+          pk_mac_lo(a[c][0], w01, x[k / 2]);
+          pk_mac_lo(a[c][1], w23, x[k / 2]);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      key = key * 16u + (a[c][0].x >= 0.0f ? 8u : 0u) + (a[c][0].y >= 0.0f ? 4u : 0u) +
+            (a[c][1].x >= 0.0f ? 2u : 0u) + (a[c][1].y >= 0.0f ? 1u : 0u);
+  };
+  int q = 0;
+  for (; q + CH <= nq; q += CH) quads(q, std::integral_constant<int, CH>{});
+  for (; q < nq; ++q) quads(q, std::integral_constant<int, 1>{});
+  key >>= (uint32_t)(4 * nq - h);  // drop the padding hyperplanes' bits
+  keys[p] = key | key_or;
+}
+
 // Any d: 32 running sums in registers (unrolled, predicated on the wave-uniform h), the row
 // streamed in 4-float chunks; per-hyperplane summation order is unchanged by the chunking.
 __global__ __launch_bounds__(256) void k_project_generic(const float* __restrict__ X, int d,
@@ -118,14 +213,22 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
                     const float* W, int h, uint32_t key_or, hipStream_t s) {
   if (n == 0) return;
   const dim3 grid((n + 255) / 256), block(256);
-  static const bool staged = [] {
-    const char* e = getenv("KLSH_PROJECT_STAGED");
-    return e && e[0] == '1';
+  // KLSH_PROJECT: "pk2" (default: packed f32, 8 chains) | "pk" (4 chains) | "scalar" | "staged"
+  static const int variant = [] {
+    const char* e = getenv("KLSH_PROJECT");
+    if (!e) return 1;
+    const std::string v(e);
+    return v == "pk" ? 0 : v == "scalar" ? 2 : v == "staged" ? 3 : 1;
   }();
+  const bool staged = variant == 3;
   switch (r.d) {
 #define KLSH_PROJECT_CASE(DD)                                                                    \
   case DD:                                                                                     \
-    if (staged)                                                                                \
+    if (variant == 0)                                                                          \
+      k_project_pk<DD, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
+    else if (variant == 1)                                                                     \
+      k_project_pk<DD, 2><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
+    else if (staged)                                                                           \
       k_project<DD, true><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
     else                                                                                       \
       k_project<DD, false><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);    \

@@ -1,0 +1,207 @@
+// gfx950 kernels of the sharded Cluster() loop: key-range ownership, the
+// (key, slot) exchange buffers, and the merge deltas that keep every rank's replica of the rows
+// identical.  No arithmetic of the reference lives here — only integer bookkeeping and copies.
+#include <hip/hip_runtime.h>
+
+#include "klsh_device.cuh"
+
+namespace klsh {
+
+// ------------------------------------------------------------------------- key-range bins -----
+__global__ __launch_bounds__(256) void k_bin_hist(const uint32_t* __restrict__ keys, uint32_t n,
+                                                  int shift, uint32_t nbins,
+                                                  uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[1u << kMaxBinBits];
+  for (uint32_t b = threadIdx.x; b < nbins; b += 256) h[b] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
+    atomicAdd(&h[keys[i] >> shift], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += 256)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+void launch_bin_hist(const uint32_t* keys, uint32_t n, int shift, uint32_t nbins, uint32_t* hist,
+                     hipStream_t s) {
+  (void)hipMemsetAsync(hist, 0, sizeof(uint32_t) * nbins, s);
+  if (n == 0) return;
+  const uint32_t g = (uint32_t)std::min<uint64_t>(1024, (n + 255) / 256);
+  k_bin_hist<<<g, 256, 0, s>>>(keys, n, shift, nbins, hist);
+}
+
+// One workgroup.  A bin's owner is decided by the midpoint of its row range in the global bin
+// order, so ranges are contiguous and balanced to within one bin; every rank computes the same.
+__global__ __launch_bounds__(1024) void k_bin_split(const uint32_t* __restrict__ hist_all,
+                                                    int world, uint32_t nbins, uint64_t total,
+                                                    uint32_t* __restrict__ owner,
+                                                    uint32_t* __restrict__ cntmat) {
+  __shared__ uint32_t tot[1u << kMaxBinBits];
+  __shared__ uint32_t own[1u << kMaxBinBits];
+  __shared__ uint32_t mat[kMaxRanks * kMaxRanks];
+  for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
+    uint32_t t = 0;
+    for (int r = 0; r < world; ++r) t += hist_all[(size_t)r * nbins + b];
+    tot[b] = t;
+  }
+  for (uint32_t k = threadIdx.x; k < (uint32_t)(world * world); k += 1024) mat[k] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 4096 bins: a serial prefix is a few microseconds
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < nbins; ++b) {
+      const uint64_t mid2 = 2 * run + tot[b];  // twice the midpoint
+      uint64_t o = total ? (mid2 * (uint64_t)world) / (2 * total) : 0;
+      own[b] = (uint32_t)(o >= (uint64_t)world ? world - 1 : o);
+      run += tot[b];
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
+    owner[b] = own[b];
+    for (int g = 0; g < world; ++g) {
+      const uint32_t c = hist_all[(size_t)g * nbins + b];
+      if (c) atomicAdd(&mat[g * world + own[b]], c);
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < (uint32_t)(world * world); k += 1024) cntmat[k] = mat[k];
+}
+
+void launch_bin_split(const uint32_t* hist_all, int world, uint32_t nbins, uint64_t total,
+                      uint32_t* owner, uint32_t* cntmat, hipStream_t s) {
+  k_bin_split<<<1, 1024, 0, s>>>(hist_all, world, nbins, total, owner, cntmat);
+}
+
+// --------------------------------------------------------------------- exchange buffers -----
+__global__ __launch_bounds__(256) void k_dest(const uint32_t* __restrict__ keys, uint32_t n,
+                                              int shift, const uint32_t* __restrict__ owner,
+                                              uint32_t* __restrict__ dest,
+                                              uint32_t* __restrict__ idx) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  dest[i] = owner[keys[i] >> shift];
+  idx[i] = i;
+}
+
+void launch_dest(const uint32_t* keys, uint32_t n, int shift, const uint32_t* owner,
+                 uint32_t* dest, uint32_t* idx, hipStream_t s) {
+  if (n) k_dest<<<(n + 255) / 256, 256, 0, s>>>(keys, n, shift, owner, dest, idx);
+}
+
+__global__ __launch_bounds__(256) void k_pack_pairs(const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ slots,
+                                                    const uint32_t* __restrict__ idx, uint32_t n,
+                                                    uint2* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = idx[i];
+  out[i] = make_uint2(keys[j], slots[j]);
+}
+
+void launch_pack_pairs(const uint32_t* keys, const uint32_t* slots, const uint32_t* idx,
+                       uint32_t n, uint2* out, hipStream_t s) {
+  if (n) k_pack_pairs<<<(n + 255) / 256, 256, 0, s>>>(keys, slots, idx, n, out);
+}
+
+__global__ __launch_bounds__(256) void k_unpack_pairs(const uint2* __restrict__ in, uint32_t n,
+                                                      uint32_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ slots,
+                                                      const uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ prev) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint2 v = in[i];
+  keys[i] = v.x;
+  slots[i] = v.y;
+  prev[v.y] = cnt[v.y];
+}
+
+void launch_unpack_pairs(const uint2* in, uint32_t n, uint32_t* keys, uint32_t* slots,
+                         const uint32_t* cnt, uint32_t* prev, hipStream_t s) {
+  if (n) k_unpack_pairs<<<(n + 255) / 256, 256, 0, s>>>(in, n, keys, slots, cnt, prev);
+}
+
+// ------------------------------------------------------------------------------- deltas -----
+struct SrcDirty {
+  const uint32_t* surv;
+  const uint32_t* cnt;
+  const uint32_t* prev;
+  __device__ uint32_t operator()(uint32_t i) const {
+    const uint32_t s = surv[i];
+    return cnt[s] != prev[s] ? 1u : 0u;
+  }
+};
+struct DstGather {
+  const uint32_t* surv;
+  uint32_t* out;
+  __device__ void operator()(uint32_t i, uint32_t prefix, uint32_t v) const {
+    if (v) out[prefix] = surv[i];
+  }
+};
+
+void launch_delta_select(const uint32_t* surv, uint32_t n, const uint32_t* cnt,
+                         const uint32_t* prev, uint32_t* delta_slots, uint32_t* tile_sums,
+                         Counters* ctr, hipStream_t s) {
+  device_scan(SrcDirty{surv, cnt, prev}, DstGather{surv, delta_slots}, n, tile_sums,
+              &ctr->n_delta, s);
+}
+
+// One thread per record word: consecutive lanes write consecutive words (and read one row).
+__global__ __launch_bounds__(256) void k_delta_pack(Rows r, const uint32_t* __restrict__ ds,
+                                                    uint32_t n, uint32_t* __restrict__ rec) {
+  const uint32_t R = (uint32_t)delta_words(r.dp);
+  const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (t >= (uint64_t)n * R) return;
+  const uint32_t i = (uint32_t)(t / R), w = (uint32_t)(t % R);
+  const uint32_t s = ds[i];
+  uint32_t v;
+  switch (w) {
+    case 0: v = s; break;
+    case 1: v = r.cnt[s]; break;
+    case 2: v = r.head[s]; break;
+    case 3: v = r.tail[s]; break;
+    case 4: v = __float_as_uint(r.nrm[s]); break;
+    default: v = __float_as_uint(r.x[(size_t)s * r.dp + (w - 5)]);
+  }
+  rec[t] = v;
+}
+
+void launch_delta_pack(const Rows& r, const uint32_t* delta_slots, uint32_t n, uint32_t* rec,
+                       hipStream_t s) {
+  const uint64_t total = (uint64_t)n * (uint64_t)delta_words(r.dp);
+  if (total) k_delta_pack<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(r, delta_slots, n, rec);
+}
+
+__global__ __launch_bounds__(256) void k_delta_apply(Rows r, const uint32_t* __restrict__ rec,
+                                                     uint32_t n) {
+  const uint32_t R = (uint32_t)delta_words(r.dp);
+  const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (t >= (uint64_t)n * R) return;
+  const uint32_t i = (uint32_t)(t / R), w = (uint32_t)(t % R);
+  const uint32_t s = rec[(uint64_t)i * R];
+  const uint32_t v = rec[t];
+  switch (w) {
+    case 0: break;
+    case 1: r.cnt[s] = v; break;
+    case 2: r.head[s] = v; break;
+    case 3: r.tail[s] = v; break;
+    case 4: r.nrm[s] = __uint_as_float(v); break;
+    default: r.x[(size_t)s * r.dp + (w - 5)] = __uint_as_float(v);
+  }
+}
+
+void launch_delta_apply(const Rows& r, const uint32_t* rec, uint32_t n, hipStream_t s) {
+  const uint64_t total = (uint64_t)n * (uint64_t)delta_words(r.dp);
+  if (total) k_delta_apply<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(r, rec, n);
+}
+
+__global__ __launch_bounds__(256) void k_min_u32(uint32_t* __restrict__ a,
+                                                 const uint32_t* __restrict__ b, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+  if (i < n) a[i] = min(a[i], b[i]);
+}
+
+void launch_min_u32(uint32_t* a, const uint32_t* b, size_t n, hipStream_t s) {
+  if (n) k_min_u32<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a, b, n);
+}
+
+}  // namespace klsh
