@@ -193,6 +193,8 @@ def main():
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "none"])
     ap.add_argument("--mode", default="sharded", choices=["sharded", "replicas"],
                     help="N>1: one problem sharded over the ranks (C3) or one problem per rank")
+    ap.add_argument("--shard1", action="store_true",
+                    help="profiling only: run the sharded loop on one GPU (in-process group of 1)")
     ap.add_argument("--iterations", type=int, default=0,
                     help="profiling only: override the config's -I (the metric is then not C2's)")
     args = ap.parse_args()
@@ -215,6 +217,8 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(rank, world, uid[0])
         log(f"rank {rank}/{world}: RCCL group up")
+    elif args.shard1:
+        _native.comm_init_local([eng])
     counter0, kept, _ = prepare(eng, n0, d, seed=11 if sharded else 11 + rank)
 
     def step():

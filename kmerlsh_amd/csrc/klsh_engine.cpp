@@ -129,7 +129,8 @@ struct klsh_ctx {
   klsh::Comm* comm = nullptr;
   uint2* sbuf = nullptr;       // (key, slot) pairs grouped by destination rank
   uint2* rbuf = nullptr;       // (key, slot) pairs received, in source-rank order
-  uint32_t* cprev = nullptr;   // [slots] member counts before this iteration's merge
+  uint32_t* mark = nullptr;    // [slots] iteration stamp of the last rewrite (in-place kernels)
+  uint32_t stamp = 0;
   uint32_t* dslots = nullptr;  // survivors rewritten by a merge (this rank)
   uint32_t* bins = nullptr;    // [4096] key-bin histogram of this rank
   uint32_t* bins_all = nullptr;
@@ -148,7 +149,7 @@ struct klsh_ctx {
   int rank() const { return comm ? comm->rank : 0; }
 
   void release_shard() {
-    dfree(sbuf); dfree(rbuf); dfree(cprev); dfree(dslots); dfree(bins); dfree(bins_all);
+    dfree(sbuf); dfree(rbuf); dfree(mark); dfree(dslots); dfree(bins); dfree(bins_all);
     dfree(owner); dfree(cntmat); dfree(small); dfree(drec); dfree(drec_all);
     if (h_small) (void)hipHostFree(h_small);
     h_small = nullptr;
@@ -162,7 +163,7 @@ struct klsh_ctx {
     const uint64_t s = std::max<uint64_t>(cap_slots, 1);
     const size_t nb = (size_t)1 << klsh::kMaxBinBits;
     int e = 0;
-    if ((e = dalloc(&sbuf, s)) || (e = dalloc(&rbuf, s)) || (e = dalloc(&cprev, s)) ||
+    if ((e = dalloc(&sbuf, s)) || (e = dalloc(&rbuf, s)) || (e = dalloc(&mark, s)) ||
         (e = dalloc(&dslots, s)) || (e = dalloc(&bins, nb)) || (e = dalloc(&bins_all, nb * W)) ||
         (e = dalloc(&owner, nb)) || (e = dalloc(&cntmat, (size_t)W * W)) ||
         (e = dalloc(&small, (size_t)(W + 1) * 4))) {
@@ -174,6 +175,11 @@ struct klsh_ctx {
       release_shard();
       return fail(KLSH_E_NOMEM, "pinned exchange buffer");
     }
+    if (hipMemset(mark, 0, sizeof(uint32_t) * s) != hipSuccess) {
+      release_shard();
+      return fail(KLSH_E_HIP, "mark init");
+    }
+    stamp = 0;
     shard_cap = s;
     return 0;
   }
@@ -524,11 +530,10 @@ int klsh_restore(klsh_ctx* ctx) {
 }
 
 // Merge + compaction of one iteration's sorted runs (fk/fv, n positions, in place on fv) into
-// `out`; with `prev` (sharded loop) also the list of survivors a merge rewrote (merge deltas).
+// `out` (with ctx->mw.dlist set, the merge kernels also list the survivors they rewrote).
 // Ends with the counters on the host: total (survivors), n_over (oversize runs), n_delta.
 static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
-                      int bucket_thr, uint32_t* out, const uint32_t* prev, klsh_stats* st,
-                      bool timed) {
+                      int bucket_thr, uint32_t* out, klsh_stats* st, bool timed) {
   hipStream_t s = ctx->stream;
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
   klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->mw, ctx->ctr, s);
@@ -537,10 +542,6 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
-  if (prev) {
-    klsh::launch_delta_select(out, n, ctx->rows.cnt, prev, ctx->dslots, ctx->tile_sums, ctx->ctr, s);
-    KLSH_HIP(hipGetLastError());
-  }
   if (int e = ctx->sync_counters()) return e;
   if (timed && st) {
     st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
@@ -563,11 +564,11 @@ static int oversize_runs(klsh_ctx* ctx, std::vector<uint2>* over, uint64_t* hype
 }
 
 // nestedCluster (cluster.cc:286-288 -> :89-178) for each oversize run, ascending, drawing
-// hyperplanes from *rng_counter on; then the survivors are compacted again into `out` (and the
-// delta list rebuilt with `prev`).  Ends with the counters on the host.
+// hyperplanes from *rng_counter on; then the survivors are compacted again into `out`.  Ends with
+// the counters on the host.
 static int merge_nested(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
                         const std::vector<uint2>& over, uint32_t seed_base, uint64_t* rng_counter,
-                        uint32_t* out, const uint32_t* prev, klsh_stats* st) {
+                        uint32_t* out, klsh_stats* st) {
   hipStream_t s = ctx->stream;
   for (uint32_t oi = 0; oi < (uint32_t)over.size(); ++oi) {
     const uint32_t p = over[oi].x, b = over[oi].y;
@@ -597,10 +598,6 @@ static int merge_nested(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, f
   }
   klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
   KLSH_HIP(hipGetLastError());
-  if (prev) {
-    klsh::launch_delta_select(out, n, ctx->rows.cnt, prev, ctx->dslots, ctx->tile_sums, ctx->ctr, s);
-    KLSH_HIP(hipGetLastError());
-  }
   return ctx->sync_counters();
 }
 
@@ -611,12 +608,12 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
                              int bucket_thr, uint32_t seed_base, uint64_t* rng_counter,
                              klsh_stats* st, bool timed) {
   uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
-  if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, nullptr, st, timed)) return e;
+  if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, st, timed)) return e;
   if (ctx->h_ctr->n_over > 0) {
     std::vector<uint2> over;
     uint64_t hyp = 0;
     if (int e = oversize_runs(ctx, &over, &hyp)) return e;
-    if (int e = merge_nested(ctx, fk, fv, n, thr, over, seed_base, rng_counter, out, nullptr, st))
+    if (int e = merge_nested(ctx, fk, fv, n, thr, over, seed_base, rng_counter, out, st))
       return e;
   }
   if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
@@ -732,7 +729,7 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
                                roff.data(), s);
         }))
       return comm_fail("pair all-to-all");
-    klsh::launch_unpack_pairs(ctx->rbuf, m_g, ctx->keys, ctx->alt, ctx->rows.cnt, ctx->cprev, s);
+    klsh::launch_unpack_pairs(ctx->rbuf, m_g, ctx->keys, ctx->alt, s);
     KLSH_HIP(hipEventRecord(ctx->ev[6], s));
 
     // 3. bucket order of my key range, merge, compaction, delta list
@@ -742,9 +739,14 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
     KLSH_HIP(hipGetLastError());
     KLSH_HIP(hipEventRecord(ctx->ev[5], s));
     uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
-    if (int e = merge_main(ctx, fk, fv, m_g, threshold, bucket_size_threshold, out, ctx->cprev, st,
-                           true))
-      return e;
+    ctx->mw.dlist = ctx->dslots;  // the merge kernels list the survivors they rewrite
+    ctx->mw.mark = ctx->mark;
+    ctx->mw.stamp = ++ctx->stamp;
+    const int rc_merge = merge_main(ctx, fk, fv, m_g, threshold, bucket_size_threshold, out, st, true);
+    if (rc_merge) {
+      ctx->mw.dlist = nullptr;
+      return rc_merge;
+    }
     std::vector<uint2> over;
     uint64_t my_hyp = 0;
     if (int e = oversize_runs(ctx, &over, &my_hyp)) return e;
@@ -775,9 +777,11 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
     if (any_over) {
       uint64_t rng = *rng_counter + hyp_before;
       if (!over.empty()) {
-        if (int e = merge_nested(ctx, fk, fv, m_g, threshold, over, seed_base, &rng, out,
-                                 ctx->cprev, st))
-          return e;
+        const int rc_nested = merge_nested(ctx, fk, fv, m_g, threshold, over, seed_base, &rng, out, st);
+        if (rc_nested) {
+          ctx->mw.dlist = nullptr;
+          return rc_nested;
+        }
       }
       *rng_counter += hyp_all;
       if (int e = exchange_counters(ctx->h_ctr->total, ctx->h_ctr->n_delta, 0, 0)) return e;
@@ -786,6 +790,8 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
         ndel[r] = ctx->h_small[4 * r + 1];
       }
     }
+
+    ctx->mw.dlist = nullptr;
 
     // 5. merge deltas to every replica
     uint64_t nd_all = 0;
@@ -852,7 +858,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   klsh_stats* st = stats ? stats : &local;
   memset(st, 0, sizeof(*st));
   st->world = (uint64_t)ctx->world();
-  if (ctx->world() > 1)
+  if (ctx->comm)  // any bound group, world 1 included (measures the sharded machinery alone)
     return cluster_sharded(ctx, min_similarity, iterations, bucket_size_threshold, seed_base,
                            rng_counter, nt_trace, st);
   const double t_start = now_ms();

@@ -44,6 +44,12 @@ struct MergeWork {
   uint2* huge;                     // (start, length) of runs for k_merge_wave
   uint2* over;                     // (start, length) of oversize runs
   uint32_t* tile_sums;
+  // Sharded loop only (nullptr otherwise): every survivor a merge rewrote is appended to dlist
+  // (ctr->n_delta entries, any order, each slot once); mark[slot] == stamp dedupes the kernels
+  // that merge in place (stamp: unique per iteration, never reused by a context).
+  uint32_t* dlist;
+  uint32_t* mark;
+  uint32_t stamp;
 };
 
 // Row state, structure-of-arrays, one entry per slot (a slot is a row of the loaded matrix;
@@ -128,14 +134,9 @@ void launch_dest(const uint32_t* keys, uint32_t n, int shift, const uint32_t* ow
 // out[i] = (keys[idx[i]], slots[idx[i]]).
 void launch_pack_pairs(const uint32_t* keys, const uint32_t* slots, const uint32_t* idx,
                        uint32_t n, uint2* out, hipStream_t s);
-// keys[i] = in[i].x, slots[i] = in[i].y; prev[slots[i]] = cnt[slots[i]] (member counts before
-// the merge: a survivor whose count changed was rewritten).
+// keys[i] = in[i].x, slots[i] = in[i].y.
 void launch_unpack_pairs(const uint2* in, uint32_t n, uint32_t* keys, uint32_t* slots,
-                         const uint32_t* cnt, uint32_t* prev, hipStream_t s);
-// delta_slots[0..ctr->n_delta) = survivors s (in order) with cnt[s] != prev[s].
-void launch_delta_select(const uint32_t* surv, uint32_t n, const uint32_t* cnt,
-                         const uint32_t* prev, uint32_t* delta_slots, uint32_t* tile_sums,
-                         Counters* ctr, hipStream_t s);
+                         hipStream_t s);
 // Delta records, stride 5 + dp words: slot, cnt, head, tail, nrm bits, row[dp].
 __host__ __device__ inline int delta_words(int dp) { return 5 + dp; }
 void launch_delta_pack(const Rows& r, const uint32_t* delta_slots, uint32_t n, uint32_t* rec,

@@ -55,6 +55,27 @@ __device__ __forceinline__ uint64_t lanes_below(uint32_t lane) {
   return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
+// Wave-aggregated append of `slot` for the lanes with `pred` (all lanes of the wave must call).
+__device__ __forceinline__ void append_slot(bool pred, uint32_t slot, uint32_t* list,
+                                            uint32_t* counter) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0ull) return;
+  const uint32_t lane = __lane_id();
+  const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = shfl32(base, leader);
+  if (pred) list[base + (uint32_t)__popcll(m & lanes_below(lane))] = slot;
+}
+
+// In-place kernels: record `slot` as rewritten once per iteration.
+__device__ __forceinline__ void mark_dirty(uint32_t slot, const MergeWork& w, Counters* ctr) {
+  if (w.dlist && w.mark[slot] != w.stamp) {
+    w.mark[slot] = w.stamp;
+    w.dlist[atomicAdd(&ctr->n_delta, 1u)] = slot;
+  }
+}
+
 template <int D>
 __device__ __forceinline__ float dot_reg_lds(const float (&a)[D], const float* b) {
   float s = 0.0f;
@@ -145,7 +166,7 @@ __device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucke
 template <int G, int D>
 __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
                                             uint32_t* slots, const Decider& dc, const Rows& r,
-                                            float* lds) {
+                                            float* lds, uint32_t* dlist, Counters* ctr) {
   constexpr int ST = D + 4;  // padded row stride: 16 lanes of a ds_read_b128 hit distinct banks
   const uint32_t lane = threadIdx.x;
   const uint32_t g = lane & (G - 1);
@@ -268,6 +289,7 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
       r.cnt[slot] = cnt;
       r.head[slot] = hd;
     }
+    if (dlist) append_slot(valid && alive && dirty, slot, dlist, &ctr->n_delta);
     if (valid && !alive) r.cnt[slot] = 0u;
     lds_fence();
   }
@@ -320,7 +342,7 @@ __global__ __launch_bounds__(1024) void k_classify(const uint32_t* __restrict__ 
 template <int G, int D>
 __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ list, int cls,
                                                     uint32_t* __restrict__ slots, Decider dc,
-                                                    Rows r, Counters* ctr) {
+                                                    Rows r, Counters* ctr, uint32_t* dlist) {
   __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
   constexpr uint32_t NG = 64 / G;
   const uint32_t n = __hip_atomic_load(&ctr->n_cls[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -336,7 +358,7 @@ __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ li
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
     const uint32_t slot_next = g < e_next.y ? slots[e_next.x + g] : 0u;
     const uint2 e_next2 = entry(bi + 2 * gridDim.x);
-    merge_batch<G, D>(e.x, e.y, slot, slots, dc, r, lds);
+    merge_batch<G, D>(e.x, e.y, slot, slots, dc, r, lds, dlist, ctr);
     e = e_next;
     slot = slot_next;
     e_next = e_next2;
@@ -362,7 +384,7 @@ struct BigLayout {
 template <int D, int RB, int NT, bool ROWS_LDS>
 __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list, int cls,
                                                   uint32_t* __restrict__ slots, Decider dc,
-                                                  Rows r, Counters* ctr) {
+                                                  Rows r, Counters* ctr, uint32_t* dlist) {
   using L = BigLayout<D, RB, ROWS_LDS>;
   constexpr int ST = L::ST, W = L::W, NW = NT / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -546,11 +568,17 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
       }
       // write back
       for (uint32_t q = lane; q < b; q += 64) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
-      for (uint32_t q = lane; q < size; q += 64) {
-        const uint32_t y = pos2row[q];
-        r.nrm[slot[y]] = nrm[y];
-        r.cnt[slot[y]] = cnt[y];
-        r.head[slot[y]] = hd[y];
+      for (uint32_t q0 = 0; q0 < size; q0 += 64) {  // uniform trip count (ballot inside)
+        const uint32_t q = q0 + lane;
+        bool rewritten = false;
+        if (q < size) {
+          const uint32_t y = pos2row[q];
+          rewritten = r.cnt[slot[y]] != cnt[y];  // every merge into a row raises its count
+          r.nrm[slot[y]] = nrm[y];
+          r.cnt[slot[y]] = cnt[y];
+          r.head[slot[y]] = hd[y];
+        }
+        if (dlist) append_slot(rewritten, q < size ? slot[pos2row[q]] : 0u, dlist, &ctr->n_delta);
       }
     }
     __syncthreads();
@@ -564,7 +592,7 @@ template <int D>
 __global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ list,
                                                    const uint32_t* count_ptr,
                                                    uint32_t* __restrict__ slots, Decider dc,
-                                                   Rows r) {
+                                                   Rows r, MergeWork w, Counters* ctr) {
   extern __shared__ __attribute__((aligned(16))) float sx[];  // consensus row for the norm
   const uint32_t lane = threadIdx.x;
   const uint32_t count = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -628,6 +656,7 @@ __global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ lis
           for (int kk = 0; kk < d; ++kk) nn = nn + sx[kk] * sx[kk];
           r.nrm[sj] = nn;
           link_members(r, si, sj);
+          mark_dirty(sj, w, ctr);
           s[i] = s[size - 1];
         }
         __syncthreads();
@@ -687,6 +716,7 @@ __global__ __launch_bounds__(256) void k_merge_lane_generic(const uint32_t* __re
         }
         r.nrm[sj] = nn;
         link_members(r, si, sj);
+        mark_dirty(sj, w, ctr);
         s[i] = s[size - 1];
         --size;
       } else {
@@ -748,7 +778,7 @@ static void launch_big(const MergeWork& w, int c, uint32_t* slots, const Decider
   (void)lds_ok;
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
   const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
-  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr);
+  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist);
 }
 
 template <int D>
@@ -760,17 +790,17 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   auto grid = [&](int c, uint32_t per_wave) {
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
-  k_merge_group<2, D><<<grid(0, 32), 64, 0, s>>>(w.cls[0], 0, slots, dc, r, ctr);
-  k_merge_group<4, D><<<grid(1, 16), 64, 0, s>>>(w.cls[1], 1, slots, dc, r, ctr);
-  k_merge_group<8, D><<<grid(2, 8), 64, 0, s>>>(w.cls[2], 2, slots, dc, r, ctr);
-  k_merge_group<16, D><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, dc, r, ctr);
-  k_merge_group<32, D><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, dc, r, ctr);
-  k_merge_group<64, D><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, dc, r, ctr);
+  k_merge_group<2, D><<<grid(0, 32), 64, 0, s>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
+  k_merge_group<4, D><<<grid(1, 16), 64, 0, s>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
+  k_merge_group<8, D><<<grid(2, 8), 64, 0, s>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
+  k_merge_group<16, D><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
+  k_merge_group<32, D><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
+  k_merge_group<64, D><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
   launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, s);
   launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, s);
   launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, s);
   const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 1] + 1) + 1);
-  k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r);
+  k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
 }
 
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
@@ -788,7 +818,7 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
       const uint32_t g1 = (uint32_t)std::min<uint64_t>(4096, (n + 255) / 256);
       k_merge_lane_generic<<<g1, 256, 0, s>>>(w.seg, hi, bucket_thr, slots, dc, r, w, ctr);
       const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / 65 + 1);
-      k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r);
+      k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
     }
   }
 }

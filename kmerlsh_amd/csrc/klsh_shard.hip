@@ -29,46 +29,51 @@ void launch_bin_hist(const uint32_t* keys, uint32_t n, int shift, uint32_t nbins
   k_bin_hist<<<g, 256, 0, s>>>(keys, n, shift, nbins, hist);
 }
 
-// One workgroup.  A bin's owner is decided by the midpoint of its row range in the global bin
-// order, so ranges are contiguous and balanced to within one bin; every rank computes the same.
-__global__ __launch_bounds__(1024) void k_bin_split(const uint32_t* __restrict__ hist_all,
-                                                    int world, uint32_t nbins, uint64_t total,
-                                                    uint32_t* __restrict__ owner,
-                                                    uint32_t* __restrict__ cntmat) {
-  __shared__ uint32_t tot[1u << kMaxBinBits];
-  __shared__ uint32_t own[1u << kMaxBinBits];
+// One workgroup of 256 lanes, 16 bins each.  A bin's owner is decided by the midpoint of its row
+// range in the global bin order, so ranges are contiguous and balanced to within one bin; every
+// rank computes the same.
+__global__ __launch_bounds__(256) void k_bin_split(const uint32_t* __restrict__ hist_all,
+                                                   int world, uint32_t nbins, uint64_t total,
+                                                   uint32_t* __restrict__ owner,
+                                                   uint32_t* __restrict__ cntmat) {
+  constexpr uint32_t PER = (1u << kMaxBinBits) / 256;
   __shared__ uint32_t mat[kMaxRanks * kMaxRanks];
-  for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
+  for (uint32_t k = threadIdx.x; k < (uint32_t)(world * world); k += 256) mat[k] = 0;
+  const uint32_t b0 = threadIdx.x * PER;
+  uint32_t tot[PER];
+  uint32_t acc = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < PER; ++j) {
     uint32_t t = 0;
-    for (int r = 0; r < world; ++r) t += hist_all[(size_t)r * nbins + b];
-    tot[b] = t;
+    if (b0 + j < nbins)
+      for (int r = 0; r < world; ++r) t += hist_all[(size_t)r * nbins + b0 + j];
+    tot[j] = t;
+    acc += t;
   }
-  for (uint32_t k = threadIdx.x; k < (uint32_t)(world * world); k += 1024) mat[k] = 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {  // 4096 bins: a serial prefix is a few microseconds
-    uint64_t run = 0;
-    for (uint32_t b = 0; b < nbins; ++b) {
-      const uint64_t mid2 = 2 * run + tot[b];  // twice the midpoint
-      uint64_t o = total ? (mid2 * (uint64_t)world) / (2 * total) : 0;
-      own[b] = (uint32_t)(o >= (uint64_t)world ? world - 1 : o);
-      run += tot[b];
+  uint32_t block_total;
+  uint64_t run = block_excl_scan_256(acc, &block_total);  // rows in bins before b0
+#pragma unroll
+  for (uint32_t j = 0; j < PER; ++j) {
+    const uint32_t b = b0 + j;
+    if (b < nbins) {
+      const uint64_t mid2 = 2 * run + tot[j];  // twice the midpoint
+      const uint64_t o = total ? (mid2 * (uint64_t)world) / (2 * total) : 0;
+      const uint32_t ow = (uint32_t)(o >= (uint64_t)world ? world - 1 : o);
+      owner[b] = ow;
+      for (int g = 0; g < world; ++g) {
+        const uint32_t c = hist_all[(size_t)g * nbins + b];
+        if (c) atomicAdd(&mat[g * world + ow], c);
+      }
     }
+    run += tot[j];
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nbins; b += 1024) {
-    owner[b] = own[b];
-    for (int g = 0; g < world; ++g) {
-      const uint32_t c = hist_all[(size_t)g * nbins + b];
-      if (c) atomicAdd(&mat[g * world + own[b]], c);
-    }
-  }
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < (uint32_t)(world * world); k += 1024) cntmat[k] = mat[k];
+  for (uint32_t k = threadIdx.x; k < (uint32_t)(world * world); k += 256) cntmat[k] = mat[k];
 }
 
 void launch_bin_split(const uint32_t* hist_all, int world, uint32_t nbins, uint64_t total,
                       uint32_t* owner, uint32_t* cntmat, hipStream_t s) {
-  k_bin_split<<<1, 1024, 0, s>>>(hist_all, world, nbins, total, owner, cntmat);
+  k_bin_split<<<1, 256, 0, s>>>(hist_all, world, nbins, total, owner, cntmat);
 }
 
 // --------------------------------------------------------------------- exchange buffers -----
@@ -104,47 +109,20 @@ void launch_pack_pairs(const uint32_t* keys, const uint32_t* slots, const uint32
 
 __global__ __launch_bounds__(256) void k_unpack_pairs(const uint2* __restrict__ in, uint32_t n,
                                                       uint32_t* __restrict__ keys,
-                                                      uint32_t* __restrict__ slots,
-                                                      const uint32_t* __restrict__ cnt,
-                                                      uint32_t* __restrict__ prev) {
+                                                      uint32_t* __restrict__ slots) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
   const uint2 v = in[i];
   keys[i] = v.x;
   slots[i] = v.y;
-  prev[v.y] = cnt[v.y];
 }
 
 void launch_unpack_pairs(const uint2* in, uint32_t n, uint32_t* keys, uint32_t* slots,
-                         const uint32_t* cnt, uint32_t* prev, hipStream_t s) {
-  if (n) k_unpack_pairs<<<(n + 255) / 256, 256, 0, s>>>(in, n, keys, slots, cnt, prev);
+                         hipStream_t s) {
+  if (n) k_unpack_pairs<<<(n + 255) / 256, 256, 0, s>>>(in, n, keys, slots);
 }
 
 // ------------------------------------------------------------------------------- deltas -----
-struct SrcDirty {
-  const uint32_t* surv;
-  const uint32_t* cnt;
-  const uint32_t* prev;
-  __device__ uint32_t operator()(uint32_t i) const {
-    const uint32_t s = surv[i];
-    return cnt[s] != prev[s] ? 1u : 0u;
-  }
-};
-struct DstGather {
-  const uint32_t* surv;
-  uint32_t* out;
-  __device__ void operator()(uint32_t i, uint32_t prefix, uint32_t v) const {
-    if (v) out[prefix] = surv[i];
-  }
-};
-
-void launch_delta_select(const uint32_t* surv, uint32_t n, const uint32_t* cnt,
-                         const uint32_t* prev, uint32_t* delta_slots, uint32_t* tile_sums,
-                         Counters* ctr, hipStream_t s) {
-  device_scan(SrcDirty{surv, cnt, prev}, DstGather{surv, delta_slots}, n, tile_sums,
-              &ctr->n_delta, s);
-}
-
 // One thread per record word: consecutive lanes write consecutive words (and read one row).
 __global__ __launch_bounds__(256) void k_delta_pack(Rows r, const uint32_t* __restrict__ ds,
                                                     uint32_t n, uint32_t* __restrict__ rec) {
