@@ -85,9 +85,6 @@ __global__ __launch_bounds__(256) void k_project(const float* __restrict__ X, in
 // one broadcast ds_read_b128 feeds 4 chains at column k; h is padded to a multiple of 4 with
 // zero hyperplanes whose bits are dropped.  CH quads (4·CH chains) run at once for ILP.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-#ifndef KLSH_PK_WAVES
-#define KLSH_PK_WAVES 4
-#endif
 
 
 // acc + w * (x, x), x one half of a register pair (op_sel picks the half; no register copies).
@@ -104,9 +101,11 @@ __device__ __forceinline__ void pk_mac_hi(f32x2& acc, f32x2 w, f32x2 x) {
       : "+v"(acc), "=&v"(t) : "v"(w), "v"(x));
 }
 
-template <int D, int CH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KLSH_PK_WAVES)))
-void k_project_pk(const float* __restrict__ X, int dp,
+// RPL rows per lane (rows p and p + 256 of the workgroup's 256 * RPL): every hyperplane read
+// from LDS feeds RPL rows — the single-row kernel is bound by the LDS broadcast reads about as
+// much as by the VALU.
+template <int D, int CH, int RPL>
+__global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X, int dp,
                                                     const uint32_t* __restrict__ slots,
                                                     uint32_t* __restrict__ keys, uint32_t n,
                                                     const float* __restrict__ W, int h,
@@ -123,50 +122,153 @@ void k_project_pk(const float* __restrict__ X, int dp,
     v.w = 4 * q + 3 < h ? W[(4 * q + 3) * dp + k] : 0.0f;
     sw[i] = v;
   }
-  const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t p0 = blockIdx.x * (256u * RPL) + threadIdx.x;
   __syncthreads();
-  if (p >= n) return;
-  f32x2 x[D / 2];  // (x[2m], x[2m+1])
-  {
-    const float4* src = reinterpret_cast<const float4*>(X + (size_t)slots[p] * dp);
+  if (p0 >= n) return;
+  f32x2 x[RPL][D / 2];  // (x[2m], x[2m+1]) of each row
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    const uint32_t pr = p0 + 256u * r;
+    const float4* src = reinterpret_cast<const float4*>(X + (size_t)slots[pr < n ? pr : p0] * dp);
 #pragma unroll
     for (int m = 0; m < D / 4; ++m) {
       const float4 v = src[m];
-      x[2 * m] = (f32x2){v.x, v.y};
-      x[2 * m + 1] = (f32x2){v.z, v.w};
+      x[r][2 * m] = (f32x2){v.x, v.y};
+      x[r][2 * m + 1] = (f32x2){v.z, v.w};
     }
   }
-  uint32_t key = 0;
+  uint32_t key[RPL];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) key[r] = 0;
   auto quads = [&](int q, auto ch) {
     constexpr int C = decltype(ch)::value;
-    f32x2 a[C][2];
+    f32x2 a[RPL][C][2];
 #pragma unroll
-    for (int c = 0; c < C; ++c) a[c][0] = a[c][1] = (f32x2){0.0f, 0.0f};
+    for (int r = 0; r < RPL; ++r)
+#pragma unroll
+      for (int c = 0; c < C; ++c) a[r][c][0] = a[r][c][1] = (f32x2){0.0f, 0.0f};
 #pragma unroll
     for (int k = 0; k < D; ++k) {
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         const float4 w = sw[(q + c) * D + k];
         const f32x2 w01 = (f32x2){w.x, w.y}, w23 = (f32x2){w.z, w.w};
-        if (k & 1) {
-          pk_mac_hi(a[c][0], w01, x[k / 2]);
-          pk_mac_hi(a[c][1], w23, x[k / 2]);
-        } else {
-          pk_mac_lo(a[c][0], w01, x[k / 2]);
-          pk_mac_lo(a[c][1], w23, x[k / 2]);
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+          if (k & 1) {
+            pk_mac_hi(a[r][c][0], w01, x[r][k / 2]);
+            pk_mac_hi(a[r][c][1], w23, x[r][k / 2]);
+          } else {
+            pk_mac_lo(a[r][c][0], w01, x[r][k / 2]);
+            pk_mac_lo(a[r][c][1], w23, x[r][k / 2]);
+          }
         }
       }
     }
 #pragma unroll
-    for (int c = 0; c < C; ++c)
-      key = key * 16u + (a[c][0].x >= 0.0f ? 8u : 0u) + (a[c][0].y >= 0.0f ? 4u : 0u) +
-            (a[c][1].x >= 0.0f ? 2u : 0u) + (a[c][1].y >= 0.0f ? 1u : 0u);
+    for (int r = 0; r < RPL; ++r)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        key[r] = key[r] * 16u + (a[r][c][0].x >= 0.0f ? 8u : 0u) +
+                 (a[r][c][0].y >= 0.0f ? 4u : 0u) + (a[r][c][1].x >= 0.0f ? 2u : 0u) +
+                 (a[r][c][1].y >= 0.0f ? 1u : 0u);
   };
   int q = 0;
   for (; q + CH <= nq; q += CH) quads(q, std::integral_constant<int, CH>{});
   for (; q < nq; ++q) quads(q, std::integral_constant<int, 1>{});
-  key >>= (uint32_t)(4 * nq - h);  // drop the padding hyperplanes' bits
-  keys[p] = key | key_or;
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    const uint32_t pr = p0 + 256u * r;
+    if (pr < n) keys[pr] = (key[r] >> (uint32_t)(4 * nq - h)) | key_or;  // drop padding bits
+  }
+}
+
+// Wide rows (d > 64 or any width without a register kernel), packed f32: every lane keeps the
+// chains of all h hyperplanes (up to 8 quads = 16 register pairs) and streams its row through
+// in 16-B pieces, in k order, so each chain is still the reference's sequential sum.  The
+// hyperplanes sit in LDS as [k][quad] float4 (one broadcast ds_read_b128 feeds 4 chains).
+template <int RPL>
+__global__ __launch_bounds__(256) void k_project_wide_pk(const float* __restrict__ X, int d,
+                                                         int dp, const uint32_t* __restrict__ slots,
+                                                         uint32_t* __restrict__ keys, uint32_t n,
+                                                         const float* __restrict__ W, int h,
+                                                         uint32_t key_or) {
+  extern __shared__ __attribute__((aligned(16))) float4 swq[];  // [dp][nq]
+  constexpr int QMAX = kMaxHyperplanes / 4;
+  const int nq = (h + 3) >> 2;
+  for (int i = threadIdx.x; i < dp * nq; i += 256) {
+    const int k = i / nq, q = i % nq;
+    float4 v;
+    v.x = 4 * q + 0 < h ? W[(4 * q + 0) * dp + k] : 0.0f;
+    v.y = 4 * q + 1 < h ? W[(4 * q + 1) * dp + k] : 0.0f;
+    v.z = 4 * q + 2 < h ? W[(4 * q + 2) * dp + k] : 0.0f;
+    v.w = 4 * q + 3 < h ? W[(4 * q + 3) * dp + k] : 0.0f;
+    swq[i] = v;
+  }
+  const uint32_t p0 = blockIdx.x * (256u * RPL) + threadIdx.x;
+  __syncthreads();
+  if (p0 >= n) return;
+  const float* x[RPL];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    const uint32_t pr = p0 + 256u * r;
+    x[r] = X + (size_t)slots[pr < n ? pr : p0] * dp;
+  }
+  f32x2 a[RPL][QMAX][2];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r)
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) a[r][q][0] = a[r][q][1] = (f32x2){0.0f, 0.0f};
+  auto column = [&](const float4* wk, const f32x2 (&xx)[RPL], bool hi) {
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      if (q < nq) {  // wave-uniform
+        const float4 w = wk[q];
+        const f32x2 w01 = (f32x2){w.x, w.y}, w23 = (f32x2){w.z, w.w};
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+          if (hi) {
+            pk_mac_hi(a[r][q][0], w01, xx[r]);
+            pk_mac_hi(a[r][q][1], w23, xx[r]);
+          } else {
+            pk_mac_lo(a[r][q][0], w01, xx[r]);
+            pk_mac_lo(a[r][q][1], w23, xx[r]);
+          }
+        }
+      }
+    }
+  };
+  const int d4 = d & ~3;
+  for (int k = 0; k < d4; k += 4) {
+    f32x2 x01[RPL], x23[RPL];
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const float4 v = *reinterpret_cast<const float4*>(x[r] + k);
+      x01[r] = (f32x2){v.x, v.y};
+      x23[r] = (f32x2){v.z, v.w};
+    }
+    column(swq + (size_t)k * nq, x01, false);
+    column(swq + (size_t)(k + 1) * nq, x01, true);
+    column(swq + (size_t)(k + 2) * nq, x23, false);
+    column(swq + (size_t)(k + 3) * nq, x23, true);
+  }
+  for (int k = d4; k < d; ++k) {
+    f32x2 xk[RPL];
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) xk[r] = (f32x2){x[r][k], x[r][k]};
+    column(swq + (size_t)k * nq, xk, false);
+  }
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    uint32_t key = 0;
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q)
+      if (q < nq)
+        key = key * 16u + (a[r][q][0].x >= 0.0f ? 8u : 0u) + (a[r][q][0].y >= 0.0f ? 4u : 0u) +
+              (a[r][q][1].x >= 0.0f ? 2u : 0u) + (a[r][q][1].y >= 0.0f ? 1u : 0u);
+    const uint32_t pr = p0 + 256u * r;
+    if (pr < n) keys[pr] = (key >> (uint32_t)(4 * nq - h)) | key_or;
+  }
 }
 
 // Any d: 32 running sums in registers (unrolled, predicated on the wave-uniform h), the row
@@ -213,33 +315,58 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
                     const float* W, int h, uint32_t key_or, hipStream_t s) {
   if (n == 0) return;
   const dim3 grid((n + 255) / 256), block(256);
-  // KLSH_PROJECT: "pk2" (default: packed f32, 8 chains) | "pk" (4 chains) | "scalar" | "staged"
+  // KLSH_PROJECT: "pk2" (default: packed f32, 8 chains, 1 row per lane) | "pk2r" (2 rows per
+  // lane; 4 for wide rows) | "pk" (4 chains) | "scalar" | "staged".  Measured on C2/C5: the extra
+  // rows per lane only add register pressure (the kernel is not LDS-read bound).
   static const int variant = [] {
     const char* e = getenv("KLSH_PROJECT");
     if (!e) return 1;
     const std::string v(e);
-    return v == "pk" ? 0 : v == "scalar" ? 2 : v == "staged" ? 3 : 1;
+    return v == "pk" ? 0 : v == "pk2r" ? 4 : v == "scalar" ? 2 : v == "staged" ? 3 : 1;
   }();
   const bool staged = variant == 3;
+  const dim3 grid2((n + 511) / 512);
   switch (r.d) {
-#define KLSH_PROJECT_CASE(DD)                                                                    \
-  case DD:                                                                                     \
-    if (variant == 0)                                                                          \
-      k_project_pk<DD, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
-    else if (variant == 1)                                                                     \
-      k_project_pk<DD, 2><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
-    else if (staged)                                                                           \
-      k_project<DD, true><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
-    else                                                                                       \
-      k_project<DD, false><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);    \
+#define KLSH_PROJECT_CASE(DD)                                                                     \
+  case DD:                                                                                      \
+    if (variant == 4)                                                                           \
+      k_project_pk<DD, 2, 2><<<grid2, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);  \
+    else if (variant == 0)                                                                      \
+      k_project_pk<DD, 1, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);   \
+    else if (variant == 1)                                                                      \
+      k_project_pk<DD, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);   \
+    else if (staged)                                                                            \
+      k_project<DD, true><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);      \
+    else                                                                                        \
+      k_project<DD, false><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
     break;
     KLSH_PROJECT_CASE(8)
     KLSH_PROJECT_CASE(16)
     KLSH_PROJECT_CASE(32)
     KLSH_PROJECT_CASE(64)
 #undef KLSH_PROJECT_CASE
-    default:
-      k_project_generic<<<grid, block, 0, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or);
+    default: {
+      const size_t lds = sizeof(float4) * (size_t)r.dp * (size_t)((h + 3) / 4);
+      if (variant != 2 && lds <= 64 * 1024) {
+        static const bool lds_ok = [] {
+          bool ok = true;
+          for (const void* f : {reinterpret_cast<const void*>(&k_project_wide_pk<1>),
+                                reinterpret_cast<const void*>(&k_project_wide_pk<4>)})
+            ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           64 * 1024) == hipSuccess;
+          return ok;
+        }();
+        (void)lds_ok;
+        if (variant == 4)
+          k_project_wide_pk<4><<<(n + 1023) / 1024, block, lds, s>>>(r.x, r.d, r.dp, slots, keys,
+                                                                     n, W, h, key_or);
+        else
+          k_project_wide_pk<1><<<grid, block, lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h,
+                                                        key_or);
+      } else {
+        k_project_generic<<<grid, block, 0, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or);
+      }
+    }
   }
 }
 

@@ -670,60 +670,414 @@ __global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ lis
   }
 }
 
-// ------------------------------------------------------------------- widths without a -----
-// register kernel: one lane per run of 2..64 rows, the reference order directly, rows from
-// memory; longer runs go to the wave kernel.
-__global__ __launch_bounds__(256) void k_merge_lane_generic(const uint32_t* __restrict__ seg,
-                                                            uint32_t hi, int bucket_thr,
-                                                            uint32_t* __restrict__ slots,
-                                                            Decider dc, Rows r, MergeWork w,
-                                                            Counters* ctr) {
-  const uint32_t nseg = __hip_atomic_load(&ctr->n_seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int d = r.d;
-  for (uint32_t sidx = blockIdx.x * 256u + threadIdx.x; sidx < nseg; sidx += gridDim.x * 256u) {
-    const uint32_t p = seg[sidx];
-    const uint32_t b = ((sidx + 1 < nseg) ? seg[sidx + 1] : hi) - p;
-    if ((bucket_thr >= 0 && b > (uint32_t)bucket_thr) || b > 64u) {
-      if (bucket_thr >= 0 && b > (uint32_t)bucket_thr)
-        w.over[atomicAdd(&ctr->n_over, 1u)] = make_uint2(p, b);
-      else
-        w.huge[atomicAdd(&ctr->n_huge, 1u)] = make_uint2(p, b);
-      continue;
+// ------------------------------------------------------------------ wide rows (any d) -----
+// Rows that do not fit in registers (d > 64, or a width without a register kernel): the same
+// G-lane group scheme, but the pairwise decisions are accumulated over 64-column chunks staged
+// through LDS (each lane's chains continue across chunks, so every dot product keeps the
+// reference's k order), and the walk's recomputations read the two rows from memory.
+constexpr int kWideKC = 64;
+
+// Columns [c0, c0 + kcp) of the 64 lanes' rows -> LDS rows (stride kWideKC + 4), coalesced:
+// 16 lanes per row, 4 rows per wave instruction.  kcp is a multiple of 4.
+__device__ __forceinline__ void stage_chunk(const float* __restrict__ X, int dp, uint32_t slot,
+                                            bool valid, int c0, int kcp, float* tile) {
+  constexpr int ST = kWideKC + 4;
+  const uint32_t lane = __lane_id();
+  const uint32_t q = lane & 15u, rsub = lane >> 4;
+  const bool col_ok = (int)(4 * q) < kcp;
+  float4 v[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const uint32_t row = it * 4 + rsub;
+    const uint32_t s = shfl32(slot, row);
+    const int ok = __shfl(valid ? 1 : 0, (int)row, 64);
+    v[it] = (ok && col_ok) ? *reinterpret_cast<const float4*>(X + (size_t)s * dp + c0 + 4 * q)
+                           : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+#pragma unroll
+  for (int it = 0; it < 16; ++it)
+    if (col_ok) *reinterpret_cast<float4*>(tile + (it * 4 + rsub) * ST + 4 * q) = v[it];
+}
+
+// s + sequential sum of a[e] * b[e], e < n, a and b in memory (16-B aligned rows)
+__device__ __forceinline__ float dot_acc_mem(float s, const float* a, const float* b, int n) {
+  int k = 0;
+  for (; k + 4 <= n; k += 4) {
+    const float4 u = *reinterpret_cast<const float4*>(a + k);
+    const float4 v = *reinterpret_cast<const float4*>(b + k);
+    s = s + u.x * v.x;
+    s = s + u.y * v.y;
+    s = s + u.z * v.z;
+    s = s + u.w * v.w;
+  }
+  for (; k < n; ++k) s = s + a[k] * b[k];
+  return s;
+}
+
+template <int N>
+__device__ __forceinline__ float dot_acc_reg(float s, const float (&a)[N], const float* b) {
+#pragma unroll
+  for (int k = 0; k < N; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(b + k);
+    s = s + a[k] * v.x;
+    s = s + a[k + 1] * v.y;
+    s = s + a[k + 2] * v.z;
+    s = s + a[k + 3] * v.w;
+  }
+  return s;
+}
+
+template <int G>
+__device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_t slot,
+                                                 uint32_t* slots, const Decider& dc,
+                                                 const Rows& r, float* tile, uint32_t* dlist,
+                                                 Counters* ctr) {
+  constexpr int ST = kWideKC + 4;
+  constexpr int NK = G / 2;  // partners per lane: k = 1 .. b/2 <= G/2
+  const uint32_t lane = threadIdx.x;
+  const uint32_t g = lane & (G - 1);
+  const uint32_t gbase = lane - g;
+  const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << (G & 63)) - 1ull) << gbase);
+  const int d = r.d, dp = r.dp;
+  const bool valid = g < b;
+  float nrm = valid ? r.nrm[slot] : 0.0f;
+  uint32_t cnt = valid ? r.cnt[slot] : 0u;
+  uint32_t hd = valid ? r.head[slot] : 0u;
+  const uint32_t tl = valid ? r.tail[slot] : 0u;
+  float sq = __builtin_sqrtf(nrm);  // distance.cc:37
+  const float* myx = r.x + (size_t)slot * dp;
+  const uint32_t bmax = wave_max(b);
+  const uint32_t half = b / 2, kmax = bmax / 2;
+  auto partner = [&](uint32_t k) {  // (g + k) mod b, for k <= b
+    const uint32_t j = g + k;
+    return j >= b ? j - b : j;
+  };
+
+  // 1. every pairwise dot product of the run, chunk by chunk (lane g vs positions g + k)
+  float acc[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) acc[k] = 0.0f;
+  for (int c0 = 0; c0 < d; c0 += kWideKC) {
+    const int n = min(kWideKC, d - c0), kcp = min(kWideKC, dp - c0);
+    lds_fence();  // the previous chunk's reads are done
+    stage_chunk(r.x, dp, slot, valid, c0, kcp, tile);
+    lds_fence();
+    const float* mine = tile + lane * ST;
+    if (n == kWideKC) {
+      float x[kWideKC];
+      load_row<kWideKC>(mine, x);
+#pragma unroll
+      for (int k = 1; k <= NK; ++k)
+        if ((uint32_t)k <= kmax && valid && (uint32_t)k <= half)
+          acc[k - 1] = dot_acc_reg<kWideKC>(acc[k - 1], x, tile + (gbase + partner(k)) * ST);
+    } else {
+#pragma unroll
+      for (int k = 1; k <= NK; ++k)
+        if ((uint32_t)k <= kmax && valid && (uint32_t)k <= half)
+          acc[k - 1] = dot_acc_mem(acc[k - 1], mine, tile + (gbase + partner(k)) * ST, n);
     }
-    uint32_t* s = slots + p;
-    uint32_t size = b, i = 1;
-    while (i < size) {
-      const uint32_t si = s[i];
-      const float* xi = r.x + (size_t)si * r.dp;
-      const float sqi = __builtin_sqrtf(r.nrm[si]);
-      uint32_t j = 0;
-      for (; j < i; ++j) {
-        const uint32_t sj = s[j];
-        if (decide(dc, dot_mem_mem(xi, r.x + (size_t)sj * r.dp, d),
-                   sqi * __builtin_sqrtf(r.nrm[sj])))
-          break;
+  }
+  uint64_t full = 0ull;
+#pragma unroll
+  for (int k = 1; k <= NK; ++k) {
+    if ((uint32_t)k <= kmax) {  // wave-uniform
+      const uint32_t j = partner(min((uint32_t)k, b));
+      const float sj = shflf(sq, gbase + (j & (G - 1)));
+      const bool bit = valid && (uint32_t)k <= half && decide(dc, acc[k - 1], sq * sj);
+      const uint32_t src = g >= (uint32_t)k ? g - k : g + b - k;  // lane holding decide(src, g)
+      const uint32_t in = (uint32_t)__shfl((int)bit, (int)(gbase + (src & (G - 1))), 64);
+      if (valid && (uint32_t)k <= half) {
+        full |= (uint64_t)bit << j;
+        full |= (uint64_t)in << src;
       }
-      if (j < i) {
-        const uint32_t sj = s[j];
-        float* xj = r.x + (size_t)sj * r.dp;
-        const float fa = (float)(int)r.cnt[si], fb = (float)(int)r.cnt[sj];
-        const float fn = (float)(int)(r.cnt[si] + r.cnt[sj]);
-        float nn = 0.0f;
-        for (int k = 0; k < d; ++k) {
-          const float v = consensus(xi[k], fa, xj[k], fb, fn);
-          xj[k] = v;
-          nn = nn + v * v;
+    }
+  }
+
+  // 2. the walk, replayed on the bits (as merge_batch); rows live in memory
+  uint32_t rowid = g, mypos = g;
+  bool alive = valid, dirty = false;
+  uint32_t i = 1, size = b;
+  while (true) {
+    const uint64_t mybit = g < size ? (1ull << rowid) : 0ull;
+    uint64_t incl = mybit;
+#pragma unroll
+    for (uint32_t o = 1; o < (uint32_t)G; o <<= 1) {
+      const uint64_t y = shfl64(incl, lane >= o ? lane - o : lane);
+      if (g >= o) incl |= y;
+    }
+    const uint64_t frow = shfl64(full, gbase + rowid);
+    const bool hit = g >= i && g < size && (frow & (incl & ~mybit)) != 0ull;
+    const uint64_t m = __ballot(hit) & gmask;
+    if (__ballot(m != 0ull) == 0ull) break;
+    if (m != 0ull) {
+      i = (uint32_t)(__ffsll((unsigned long long)m) - 1) - gbase;
+      const uint32_t rr = shfl32(rowid, gbase + i);
+      const uint64_t fr = shfl64(frow, gbase + i);
+      const uint64_t mj = __ballot(g < i && ((fr >> rowid) & 1ull)) & gmask;
+      const uint32_t jpos = (uint32_t)(__ffsll((unsigned long long)mj) - 1) - gbase;
+      const uint32_t c = shfl32(rowid, gbase + jpos);
+      const uint32_t ca = shfl32(cnt, gbase + rr), cb = shfl32(cnt, gbase + c);
+      const uint32_t hr = shfl32(hd, gbase + rr), tr = shfl32(tl, gbase + rr);
+      const uint32_t hc = shfl32(hd, gbase + c);
+      const uint32_t slot_r = shfl32(slot, gbase + rr), slot_c = shfl32(slot, gbase + c);
+      const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+      const float* xr = r.x + (size_t)slot_r * dp;
+      float* xc = r.x + (size_t)slot_c * dp;
+      for (int k = (int)g; k < d; k += G) xc[k] = consensus(xr[k], fa, xc[k], fb, fn);
+      lds_fence();  // the new row c is visible to the group's lanes
+      if (g == rr) alive = false;
+      if (g == 0) r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
+      const uint32_t last = shfl32(rowid, gbase + size - 1);  // swap-remove
+      if (g == i) rowid = last;
+      if (g == last) mypos = i;
+      --size;
+      // lane c: its exact sequential norm; rows still to be visited: their dot with row c
+      const bool todo = alive && mypos >= i && mypos < size;
+      float dot = 0.0f;
+      if (g == c || todo) dot = dot_acc_mem(0.0f, myx, xc, d);
+      if (g == c) {
+        nrm = dot;
+        sq = __builtin_sqrtf(dot);
+        cnt = ca + cb;
+        hd = hr;
+        dirty = true;
+      }
+      const float sc = shflf(sq, gbase + c);
+      if (todo) full = decide(dc, dot, sq * sc) ? (full | (1ull << c)) : (full & ~(1ull << c));
+    }
+  }
+
+  // 3. write back
+  const uint32_t pos_slot = shfl32(slot, gbase + rowid);
+  if (valid) slots[p + g] = g < size ? pos_slot : kInvalid;
+  if (valid && alive && dirty) {
+    r.nrm[slot] = nrm;
+    r.cnt[slot] = cnt;
+    r.head[slot] = hd;
+  }
+  if (dlist) append_slot(valid && alive && dirty, slot, dlist, &ctr->n_delta);
+  if (valid && !alive) r.cnt[slot] = 0u;
+  lds_fence();
+}
+
+template <int G>
+__global__ __launch_bounds__(64) void k_merge_group_wide(const uint2* __restrict__ list, int cls,
+                                                         uint32_t* __restrict__ slots, Decider dc,
+                                                         Rows r, Counters* ctr, uint32_t* dlist) {
+  __shared__ __attribute__((aligned(16))) float tile[64 * (kWideKC + 4)];
+  constexpr uint32_t NG = 64 / G;
+  const uint32_t n = __hip_atomic_load(&ctr->n_cls[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nb = (n + NG - 1) / NG;
+  const uint32_t g = threadIdx.x & (G - 1), grp = threadIdx.x / G;
+  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
+    const uint32_t k = bi * NG + grp;
+    const uint2 e = k < n ? list[k] : make_uint2(0u, 0u);
+    const uint32_t slot = g < e.y ? slots[e.x + g] : 0u;
+    merge_batch_wide<G>(e.x, e.y, slot, slots, dc, r, tile, dlist, ctr);
+  }
+}
+
+// Runs of 65..896 rows with wide rows: one workgroup per run, the decision matrix in LDS in
+// position space (as k_merge_big).  A 64x64 decision tile is one wave's job: its 64 rows'
+// chains (one per lane, 64 columns each) run over KC-column chunks, the column block's chunk
+// staged in the wave's own LDS region and read by broadcast.
+template <int RB, int NT, int KC>
+struct BigWideLayout {
+  static constexpr int W = RB / 64;
+  static constexpr int NW = NT / 64;
+  static constexpr int STB = KC + 4;
+  static constexpr size_t tiles = 0;
+  static constexpr size_t P = tiles + sizeof(float) * NW * 64 * STB;
+  static constexpr size_t meta = P + sizeof(uint64_t) * RB * W;
+  static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 7;
+};
+
+template <int RB, int NT, int KC>
+__global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__ list, int cls,
+                                                       uint32_t* __restrict__ slots, Decider dc,
+                                                       Rows r, Counters* ctr, uint32_t* dlist) {
+  using L = BigWideLayout<RB, NT, KC>;
+  constexpr int W = L::W, NW = L::NW, STB = L::STB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* P = reinterpret_cast<uint64_t*>(smem + L::P);
+  uint32_t* slot = reinterpret_cast<uint32_t*>(smem + L::meta);
+  float* nrm = reinterpret_cast<float*>(slot + RB);
+  uint32_t* cnt = slot + 2 * RB;
+  uint32_t* hd = slot + 3 * RB;
+  uint32_t* tl = slot + 4 * RB;
+  uint32_t* pos2row = slot + 5 * RB;
+  float* sq = reinterpret_cast<float*>(slot + 6 * RB);
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  float* ctile = reinterpret_cast<float*>(smem + L::tiles) + wv * 64 * STB;  // this wave's
+  const int d = r.d, dp = r.dp;
+  const uint32_t count =
+      __hip_atomic_load(&ctr->n_big[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto row_ptr = [&](uint32_t a) -> const float* { return r.x + (size_t)slot[a] * dp; };
+
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    const uint2 e = list[li];
+    const uint32_t p = e.x, b = e.y;
+    const uint32_t nblk = (b + 63) / 64;
+    for (uint32_t a = t; a < b; a += NT) {
+      const uint32_t s = slots[p + a];
+      slot[a] = s;
+      nrm[a] = r.nrm[s];
+      sq[a] = __builtin_sqrtf(nrm[a]);
+      cnt[a] = r.cnt[s];
+      hd[a] = r.head[s];
+      tl[a] = r.tail[s];
+      pos2row[a] = a;
+    }
+    for (uint32_t a = t; a < b * (uint32_t)W; a += NT) P[a] = 0ull;
+    __syncthreads();
+
+    // decision tiles (R, C <= R), one per wave at a time
+    const uint32_t ntiles = nblk * (nblk + 1) / 2;
+    for (uint32_t ti = wv; ti < ntiles; ti += NW) {
+      uint32_t R = 0;
+      while ((R + 1) * (R + 2) / 2 <= ti) ++R;
+      const uint32_t C = ti - R * (R + 1) / 2;
+      const uint32_t a = R * 64u + lane;
+      const bool va = a < b;
+      const float* xa = va ? row_ptr(a) : nullptr;
+      const uint32_t c0 = C * 64u, c1 = min(b, c0 + 64u);
+      float acc[64];
+#pragma unroll
+      for (int c = 0; c < 64; ++c) acc[c] = 0.0f;
+      for (int k0 = 0; k0 < d; k0 += KC) {
+        const int n = min(KC, d - k0), kcp = min(KC, dp - k0);
+        lds_fence();
+        for (uint32_t q = lane; q < 64u * (uint32_t)(kcp / 4); q += 64) {
+          const uint32_t row = q / (uint32_t)(kcp / 4), e4 = q % (uint32_t)(kcp / 4);
+          if (c0 + row < c1)
+            *reinterpret_cast<float4*>(ctile + row * STB + 4 * e4) =
+                *reinterpret_cast<const float4*>(r.x + (size_t)slot[c0 + row] * dp + k0 + 4 * e4);
         }
-        r.nrm[sj] = nn;
-        link_members(r, si, sj);
-        mark_dirty(sj, w, ctr);
-        s[i] = s[size - 1];
+        lds_fence();
+        if (n == KC) {
+          float x[KC];
+#pragma unroll
+          for (int k = 0; k < KC; k += 4) {
+            const float4 v = va ? *reinterpret_cast<const float4*>(xa + k0 + k)
+                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            x[k] = v.x; x[k + 1] = v.y; x[k + 2] = v.z; x[k + 3] = v.w;
+          }
+#pragma unroll
+          for (int c = 0; c < 64; ++c)
+            if (c0 + c < c1) acc[c] = dot_acc_reg<KC>(acc[c], x, ctile + c * STB);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 64; ++c)
+            if (c0 + c < c1 && va) {
+              float s = acc[c];
+              for (int k = 0; k < n; ++k) s = s + xa[k0 + k] * ctile[c * STB + k];
+              acc[c] = s;
+            }
+        }
+      }
+      const float sa = va ? sq[a] : 0.0f;
+      uint64_t own = 0ull;
+#pragma unroll
+      for (int c = 0; c < 64; ++c) {
+        const uint32_t cc = c0 + c;
+        if (cc < c1) {  // wave-uniform
+          const bool h = va && cc < a && decide(dc, acc[c], sa * sq[cc]);
+          const uint64_t m = __ballot(h);
+          if (lane == 0 && m) atomicOr((unsigned long long*)&P[cc * W + R], (unsigned long long)m);
+          own |= (h ? 1ull : 0ull) << c;
+        }
+      }
+      if (va && own) atomicOr((unsigned long long*)&P[a * W + C], (unsigned long long)own);
+    }
+    __syncthreads();
+
+    // the walk, by wave 0 (as k_merge_big with rows in memory)
+    if (wv == 0) {
+      uint32_t i = 1, size = b;
+      while (true) {
+        uint32_t q = size;
+        for (uint32_t q0 = i; q0 < size; q0 += 64) {
+          const uint32_t qq = q0 + lane;
+          bool hit = false;
+          if (qq < size) {
+            const uint64_t* Py = P + pos2row[qq] * W;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+              const uint32_t lo = (uint32_t)k * 64u;
+              if (lo < qq) {
+                const uint64_t wk = Py[k];
+                hit |= (qq - lo >= 64u ? wk : (wk & ((1ull << (qq - lo)) - 1ull))) != 0ull;
+              }
+            }
+          }
+          const uint64_t m = __ballot(hit);
+          if (m != 0ull) {
+            q = q0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+            break;
+          }
+        }
+        if (q >= size) break;
+        i = q;
+        const uint32_t rr = pos2row[i];
+        uint64_t word = 0ull;
+        if (lane < (uint32_t)W) {
+          word = P[rr * W + lane];
+          const uint32_t lo = lane * 64u;
+          if (lo >= i) word = 0ull;
+          else if (i - lo < 64u) word &= (1ull << (i - lo)) - 1ull;
+        }
+        const uint64_t nz = __ballot(word != 0ull);
+        const uint32_t wd = (uint32_t)(__ffsll((unsigned long long)nz) - 1);
+        const uint64_t wbits = shfl64(word, wd);
+        const uint32_t j = wd * 64u + (uint32_t)(__ffsll((unsigned long long)wbits) - 1);
+        const uint32_t c = pos2row[j];
+        const uint32_t ca = cnt[rr], cb = cnt[c];
+        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+        float* xc = r.x + (size_t)slot[c] * dp;
+        const float* xr = row_ptr(rr);
+        for (int k = (int)lane; k < d; k += 64) xc[k] = consensus(xr[k], fa, xc[k], fb, fn);
+        lds_fence();
+        if (lane == 0) {
+          const float nn = dot_acc_mem(0.0f, xc, xc, d);
+          nrm[c] = nn;
+          sq[c] = __builtin_sqrtf(nn);
+          r.nxt[tl[rr]] = hd[c];  // ids_current ++ ids_candidate
+          hd[c] = hd[rr];
+          cnt[c] = ca + cb;
+          cnt[rr] = 0u;
+          pos2row[i] = pos2row[size - 1];  // swap-remove
+        }
+        lds_fence();
         --size;
-      } else {
-        ++i;
+        const float sc = sq[c];
+        const uint32_t moved = size;
+        for (uint32_t qq = i + lane; qq < size; qq += 64) {
+          const uint32_t y = pos2row[qq];
+          uint64_t* Py = P + y * W;
+          const bool bm = (Py[moved / 64] >> (moved & 63u)) & 1ull;
+          Py[moved / 64] &= ~(1ull << (moved & 63u));
+          Py[i / 64] = bm ? (Py[i / 64] | (1ull << (i & 63u))) : (Py[i / 64] & ~(1ull << (i & 63u)));
+          const float dot = dot_acc_mem(0.0f, row_ptr(y), xc, d);
+          const bool dn = decide(dc, dot, sq[y] * sc);
+          Py[j / 64] = dn ? (Py[j / 64] | (1ull << (j & 63u))) : (Py[j / 64] & ~(1ull << (j & 63u)));
+        }
+        lds_fence();
+      }
+      for (uint32_t q = lane; q < b; q += 64) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
+      for (uint32_t q0 = 0; q0 < size; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        bool rewritten = false;
+        if (q < size) {
+          const uint32_t y = pos2row[q];
+          rewritten = r.cnt[slot[y]] != cnt[y];
+          r.nrm[slot[y]] = nrm[y];
+          r.cnt[slot[y]] = cnt[y];
+          r.head[slot[y]] = hd[y];
+        }
+        if (dlist) append_slot(rewritten, q < size ? slot[pos2row[q]] : 0u, dlist, &ctr->n_delta);
       }
     }
-    for (uint32_t t = size; t < b; ++t) s[t] = kInvalid;
+    __syncthreads();
   }
 }
 
@@ -803,6 +1157,41 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
 }
 
+template <int RB, int NT, int KC>
+static void launch_big_wide(const MergeWork& w, int c, uint32_t* slots, const Decider& dc,
+                            const Rows& r, Counters* ctr, uint32_t n, hipStream_t s) {
+  using L = BigWideLayout<RB, NT, KC>;
+  static const bool lds_ok = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_big_wide<RB, NT, KC>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)L::bytes) == hipSuccess;
+  }();
+  (void)lds_ok;
+  const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
+  const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
+  k_merge_big_wide<RB, NT, KC><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist);
+}
+
+static void launch_groups_wide(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
+                               uint32_t* slots, const Decider& dc, const MergeWork& w,
+                               Counters* ctr, uint32_t n, hipStream_t s) {
+  k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
+  auto grid = [&](int c, uint32_t per_wave) {
+    return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
+  };
+  k_merge_group_wide<2><<<grid(0, 32), 64, 0, s>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<4><<<grid(1, 16), 64, 0, s>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<8><<<grid(2, 8), 64, 0, s>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<16><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<32><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<64><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
+  launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, s);
+  launch_big_wide<384, 256, 32>(w, 1, slots, dc, r, ctr, n, s);
+  launch_big_wide<896, 256, 16>(w, 2, slots, dc, r, ctr, n, s);
+  const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 1] + 1) + 1);
+  k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
+}
+
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
                   float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s) {
   if (hi <= lo) return;
@@ -814,12 +1203,7 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
     case 16: launch_groups<16>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
     case 32: launch_groups<32>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
     case 64: launch_groups<64>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
-    default: {
-      const uint32_t g1 = (uint32_t)std::min<uint64_t>(4096, (n + 255) / 256);
-      k_merge_lane_generic<<<g1, 256, 0, s>>>(w.seg, hi, bucket_thr, slots, dc, r, w, ctr);
-      const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / 65 + 1);
-      k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
-    }
+    default: launch_groups_wide(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s);
   }
 }
 

@@ -79,6 +79,11 @@ def test_pcluster_matches_reference(engine, name):
     (385, 64, 30, 0.05, 0.95), (700, 16, 50, 0.1, 0.8), (64, 8, 3, 0.2, 0.9), (3, 64, 1, 0.01, 0.9),
     (128, 64, 10, 0.05, 0.9), (129, 64, 10, 0.05, 0.9), (896, 64, 200, 0.05, 0.95),
     (897, 32, 200, 0.05, 0.95), (600, 8, 40, 0.1, 0.85), (250, 16, 1, 0.0, 0.9),
+    # wide rows (chunked kernels): every size class, widths with and without partial chunks
+    (2, 512, 1, 0.05, 0.9), (7, 512, 2, 0.05, 0.9), (33, 512, 4, 0.05, 0.9),
+    (64, 100, 5, 0.05, 0.9), (100, 512, 8, 0.05, 0.9), (300, 130, 20, 0.05, 0.9),
+    (500, 512, 30, 0.05, 0.95), (1000, 70, 60, 0.05, 0.9), (40, 13, 3, 0.1, 0.85),
+    (60, 2048, 4, 0.05, 0.9),
 ])
 def test_pcluster_run_lengths_vs_oracle(engine, oracle, b, d, groups, noise, thr):
     """Every merge path by bucket length: G-lane groups (<= 64), LDS matrix (65..384), wave (> 384)."""
@@ -169,7 +174,8 @@ def clustered(rng, n, d, groups, noise):
 @pytest.mark.parametrize("n,d,groups,iters,bthr", [
     (200000, 64, 4000, 12, 1000000),
     (100000, 32, 500, 8, 1000000),
-    (60000, 20, 300, 6, 1000000),      # generic kernels
+    (60000, 20, 300, 6, 1000000),      # wide kernels, one partial chunk
+    (30000, 512, 400, 5, 1000000),     # C5 width
     (50000, 16, 3, 3, 5000),           # nested path in every iteration
 ])
 def test_cluster_random_vs_oracle(engine, oracle, n, d, groups, iters, bthr):
