@@ -193,12 +193,16 @@ def main():
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "none"])
     ap.add_argument("--mode", default="sharded", choices=["sharded", "replicas"],
                     help="N>1: one problem sharded over the ranks (C3) or one problem per rank")
+    ap.add_argument("--phases", action="store_true",
+                    help="per-phase HIP-event timing (sort/merge/compaction); adds latency")
     ap.add_argument("--shard1", action="store_true",
                     help="profiling only: run the sharded loop on one GPU (in-process group of 1)")
     ap.add_argument("--iterations", type=int, default=0,
                     help="profiling only: override the config's -I (the metric is then not C2's)")
     args = ap.parse_args()
 
+    if args.phases:
+        os.environ["KLSH_PHASE_TIMING"] = "1"
     world, rank, local = dist_setup()
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")

@@ -145,6 +145,14 @@ struct klsh_ctx {
 
   ~klsh_ctx() { release(); }
 
+  // Per-phase HIP events (sort / merge / compaction) cost latency in every iteration — an event
+  // record on the stream is tens of microseconds in the small late iterations — so they are on
+  // only with KLSH_PHASE_TIMING=1.  The projection is always bracketed (bench.py's roofline).
+  bool phase_timing = [] {
+    const char* e = getenv("KLSH_PHASE_TIMING");
+    return e && e[0] == '1';
+  }();
+
   int world() const { return comm ? comm->world : 1; }
   int rank() const { return comm ? comm->rank : 0; }
 
@@ -220,6 +228,14 @@ struct klsh_ctx {
     h_ctr = nullptr;
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e), e = nullptr;
+    for (int i = 0; i < klsh::kMergeStreams; ++i) {
+      if (mw.join[i]) (void)hipEventDestroy(mw.join[i]);
+      if (mw.aux[i]) (void)hipStreamDestroy(mw.aux[i]);
+      mw.join[i] = nullptr;
+      mw.aux[i] = nullptr;
+    }
+    if (mw.fork) (void)hipEventDestroy(mw.fork);
+    mw.fork = nullptr;
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -357,6 +373,11 @@ klsh_ctx* klsh_create(int device, int* err) {
   c->device = device;
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
   for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  for (int i = 0; i < klsh::kMergeStreams; ++i) {
+    ok = ok && hipStreamCreateWithFlags(&c->mw.aux[i], hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&c->mw.join[i], hipEventDisableTiming) == hipSuccess;
+  }
+  ok = ok && hipEventCreateWithFlags(&c->mw.fork, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->ctr, sizeof(Counters)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) == hipSuccess;
   if (!ok) {
@@ -730,19 +751,20 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
         }))
       return comm_fail("pair all-to-all");
     klsh::launch_unpack_pairs(ctx->rbuf, m_g, ctx->keys, ctx->alt, s);
-    KLSH_HIP(hipEventRecord(ctx->ev[6], s));
+    if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[6], s));
 
     // 3. bucket order of my key range, merge, compaction, delta list
     uint32_t *fk = nullptr, *fv = nullptr;
     klsh::radix_sort(ctx->keys, ctx->alt, ctx->keys2, ctx->order, m_g, h, ctx->hist,
                      ctx->tile_sums, ctx->ctr, &fk, &fv, s);
     KLSH_HIP(hipGetLastError());
-    KLSH_HIP(hipEventRecord(ctx->ev[5], s));
+    if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[5], s));
     uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
     ctx->mw.dlist = ctx->dslots;  // the merge kernels list the survivors they rewrite
     ctx->mw.mark = ctx->mark;
     ctx->mw.stamp = ++ctx->stamp;
-    const int rc_merge = merge_main(ctx, fk, fv, m_g, threshold, bucket_size_threshold, out, st, true);
+    const int rc_merge = merge_main(ctx, fk, fv, m_g, threshold, bucket_size_threshold, out, st,
+                                    ctx->phase_timing);
     if (rc_merge) {
       ctx->mw.dlist = nullptr;
       return rc_merge;
@@ -815,7 +837,7 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
     if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
     const uint64_t N_next = std::accumulate(surv.begin(), surv.end(), (uint64_t)0);
     st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
-    st->sort_ms += elapsed(ctx->ev[6], ctx->ev[5]);
+    if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[6], ctx->ev[5]);
     st->project_launches += 1;
     st->sum_rows += N;
     st->sum_proj_bits += N * (uint64_t)h;
@@ -905,7 +927,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
     klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n, h, ctx->hist,
                      ctx->tile_sums, ctx->ctr, &fk, &fv, s);
     KLSH_HIP(hipGetLastError());
-    KLSH_HIP(hipEventRecord(ctx->ev[5], s));
+    if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[5], s));
     if (const char* path = getenv("KLSH_BUCKET_STATS")) {  // diagnostics: run-length histogram
       std::vector<uint32_t> hk(n);
       KLSH_HIP(hipMemcpyAsync(hk.data(), fk, 4 * n, hipMemcpyDeviceToHost, s));
@@ -934,10 +956,10 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
       }
     }
     if (int e = merge_and_compact(ctx, fk, fv, (uint32_t)n, threshold, bucket_size_threshold,
-                                  seed_base, rng_counter, st, true))
+                                  seed_base, rng_counter, st, ctx->phase_timing))
       return e;
     st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
-    st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
+    if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
     st->project_launches += 1;
     st->sum_rows += n;
     st->sum_proj_bits += n * (uint64_t)h;

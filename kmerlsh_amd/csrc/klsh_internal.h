@@ -50,7 +50,14 @@ struct MergeWork {
   uint32_t* dlist;
   uint32_t* mark;
   uint32_t stamp;
+  // Size classes run concurrently on kMergeStreams auxiliary streams (fork after the run
+  // classification, join before the compaction): in the late, small iterations each class kernel
+  // is one long sequential walk, and serialised walks would add up.  aux[0] == nullptr: one stream.
+  hipStream_t aux[3];
+  hipEvent_t fork;
+  hipEvent_t join[3];
 };
+constexpr int kMergeStreams = 3;
 
 // Row state, structure-of-arrays, one entry per slot (a slot is a row of the loaded matrix;
 // a merge writes the consensus into the candidate's slot, cluster.cc:70-74).

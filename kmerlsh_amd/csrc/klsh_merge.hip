@@ -371,6 +371,158 @@ __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ li
 // 64-row column block at a time for the decision phase).  The matrix is kept in POSITION space:
 // P[y] bit q = decide(row y, row at position q), so the walk's "first j < i" is a
 // find-first-set over W words, and positions that find nothing are skipped in bulk.
+// s + sequential sum of a[e] * b[e], e < n, a and b in memory (16-B aligned rows)
+__device__ __forceinline__ float dot_acc_mem(float s, const float* a, const float* b, int n) {
+  int k = 0;
+  for (; k + 4 <= n; k += 4) {
+    const float4 u = *reinterpret_cast<const float4*>(a + k);
+    const float4 v = *reinterpret_cast<const float4*>(b + k);
+    s = s + u.x * v.x;
+    s = s + u.y * v.y;
+    s = s + u.z * v.z;
+    s = s + u.w * v.w;
+  }
+  for (; k < n; ++k) s = s + a[k] * b[k];
+  return s;
+}
+
+// The walk of one 65..896-row run over its position-space decision matrix P (k_merge_big*),
+// shared by the whole workgroup: every step finds the first position q >= i whose row matches a
+// position below q (positions that find nothing change nothing), does the reference's merge
+// there, and recomputes the decisions of the rows still to be visited against the new row —
+// spread over all NT lanes (the new row's norm on one lane meanwhile).  Rows are read from
+// rowsL (LDS, stride ST) if given, else from memory; the new row is kept in LDS (cbuf).
+template <int RB, int NT>
+__device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, uint32_t* slot,
+                                         float* nrm, uint32_t* cnt, uint32_t* hd, uint32_t* tl,
+                                         uint32_t* pos2row, float* sq, float* rowsL, int ST,
+                                         float* cbuf, uint32_t* wbuf, const Rows& r,
+                                         const Decider& dc, uint32_t* slots, uint32_t* dlist,
+                                         Counters* ctr) {
+  constexpr int W = RB / 64, NW = NT / 64, KP = (RB + NT - 1) / NT;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const int d = r.d, dp = r.dp;
+  auto rowp = [&](uint32_t a) -> const float* {
+    return rowsL ? rowsL + a * ST : r.x + (size_t)slot[a] * dp;
+  };
+  uint32_t i = 1, size = b, par = 0;
+  while (true) {
+    // 1. the next position that merges
+    uint32_t q = size;
+    for (uint32_t q0 = i; q0 < size; q0 += NT) {
+      const uint32_t qq = q0 + t;
+      bool hit = false;
+      if (qq < size) {
+        const uint64_t* Py = P + pos2row[qq] * W;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const uint32_t lo = (uint32_t)k * 64u;
+          if (lo < qq) {
+            const uint64_t wk = Py[k];
+            hit |= (qq - lo >= 64u ? wk : (wk & ((1ull << (qq - lo)) - 1ull))) != 0ull;
+          }
+        }
+      }
+      const uint64_t m = __ballot(hit);
+      if (lane == 0)
+        wbuf[par * NW + wv] = m ? q0 + wv * 64u + (uint32_t)(__ffsll((unsigned long long)m) - 1)
+                                : 0xFFFFFFFFu;
+      __syncthreads();
+      uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) best = min(best, wbuf[par * NW + w]);
+      par ^= 1u;
+      if (best != 0xFFFFFFFFu) {  // block-uniform
+        q = best;
+        break;
+      }
+    }
+    if (q >= size) break;
+    i = q;
+    // 2. its first matching position j < i (every wave computes it)
+    const uint32_t rr = pos2row[i];
+    uint64_t word = 0ull;
+    if (lane < (uint32_t)W) {
+      word = P[rr * W + lane];
+      const uint32_t lo = lane * 64u;
+      if (lo >= i) word = 0ull;
+      else if (i - lo < 64u) word &= (1ull << (i - lo)) - 1ull;
+    }
+    const uint64_t nz = __ballot(word != 0ull);
+    const uint32_t wd = (uint32_t)(__ffsll((unsigned long long)nz) - 1);
+    const uint64_t wbits = shfl64(word, wd);
+    const uint32_t j = wd * 64u + (uint32_t)(__ffsll((unsigned long long)wbits) - 1);
+    const uint32_t c = pos2row[j];
+    const uint32_t ca = cnt[rr], cb = cnt[c];
+    const uint32_t hr = hd[rr], tr = tl[rr], hc = hd[c];
+    const uint32_t moved_row = pos2row[size - 1];
+    __syncthreads();  // all reads of the old state are done
+    // 3. consensus (funcAB.cc:65), current row first; member links and the swap-remove
+    const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+    float* xc = r.x + (size_t)slot[c] * dp;
+    const float* xr = rowp(rr);
+    float* lc = rowsL ? rowsL + c * ST : cbuf;  // the new row c, in LDS
+    for (int k = (int)t; k < d; k += NT) {
+      const float v = consensus(xr[k], fa, rowsL ? lc[k] : xc[k], fb, fn);
+      lc[k] = v;
+      xc[k] = v;
+    }
+    if (t == 0) {
+      r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
+      hd[c] = hr;
+      cnt[c] = ca + cb;
+      cnt[rr] = 0u;
+      pos2row[i] = moved_row;
+    }
+    __syncthreads();
+    --size;
+    const uint32_t moved = size;  // old position of the row now at i
+    // 4. dot products of the rows still to be visited with row c; row c's norm
+    float dots[KP];
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      const uint32_t qq = i + t + (uint32_t)kp * NT;
+      dots[kp] = qq < size ? dot_acc_mem(0.0f, rowp(pos2row[qq]), lc, d) : 0.0f;
+    }
+    if (t == NT - 1) {
+      const float nn = dot_acc_mem(0.0f, lc, lc, d);  // distance.cc:33-34
+      nrm[c] = nn;
+      sq[c] = __builtin_sqrtf(nn);
+    }
+    __syncthreads();
+    // 5. position-space bits: the moved row's bit goes to position i, bit j is re-decided
+    const float sc = sq[c];
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      const uint32_t qq = i + t + (uint32_t)kp * NT;
+      if (qq < size) {
+        const uint32_t y = pos2row[qq];
+        uint64_t* Py = P + y * W;
+        const bool bm = (Py[moved / 64] >> (moved & 63u)) & 1ull;
+        Py[moved / 64] &= ~(1ull << (moved & 63u));
+        Py[i / 64] = bm ? (Py[i / 64] | (1ull << (i & 63u))) : (Py[i / 64] & ~(1ull << (i & 63u)));
+        const bool dn = decide(dc, dots[kp], sq[y] * sc);
+        Py[j / 64] = dn ? (Py[j / 64] | (1ull << (j & 63u))) : (Py[j / 64] & ~(1ull << (j & 63u)));
+      }
+    }
+    __syncthreads();
+  }
+  // write back: survivors in position order, kInvalid after; metadata of the survivors
+  for (uint32_t q = t; q < b; q += NT) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
+  for (uint32_t q0 = 0; q0 < size; q0 += NT) {  // uniform trip count (ballot inside)
+    const uint32_t q = q0 + t;
+    bool rewritten = false;
+    if (q < size) {
+      const uint32_t y = pos2row[q];
+      rewritten = r.cnt[slot[y]] != cnt[y];  // every merge into a row raises its count
+      r.nrm[slot[y]] = nrm[y];
+      r.cnt[slot[y]] = cnt[y];
+      r.head[slot[y]] = hd[y];
+    }
+    if (dlist) append_slot(rewritten, q < size ? slot[pos2row[q]] : 0u, dlist, &ctr->n_delta);
+  }
+}
+
 template <int D, int RB, bool ROWS_LDS>
 struct BigLayout {
   static constexpr int ST = D + 4;
@@ -397,6 +549,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
   uint32_t* tl = slot + 4 * RB;
   uint32_t* pos2row = slot + 5 * RB;
   float* sq = reinterpret_cast<float*>(slot + 6 * RB);  // sqrtf(nrm), distance.cc:37
+  __shared__ uint32_t wbuf[2 * NW];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t count =
       __hip_atomic_load(&ctr->n_big[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -483,104 +636,8 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
     }
     __syncthreads();
 
-    // the walk, by wave 0: jump to the first position q >= i whose row matches a position
-    // below q (positions that find nothing change nothing), then do the reference's merge there.
-    if (wv == 0) {
-      uint32_t i = 1, size = b;
-      while (true) {
-        uint32_t q = size;
-        for (uint32_t q0 = i; q0 < size; q0 += 64) {
-          const uint32_t qq = q0 + lane;
-          bool hit = false;
-          if (qq < size) {
-            const uint64_t* Py = P + pos2row[qq] * W;
-#pragma unroll
-            for (int k = 0; k < W; ++k) {
-              const uint32_t lo = (uint32_t)k * 64u;
-              if (lo < qq) {
-                const uint64_t wk = Py[k];
-                hit |= (qq - lo >= 64u ? wk : (wk & ((1ull << (qq - lo)) - 1ull))) != 0ull;
-              }
-            }
-          }
-          const uint64_t m = __ballot(hit);
-          if (m != 0ull) {
-            q = q0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
-            break;
-          }
-        }
-        if (q >= size) break;
-        i = q;
-        const uint32_t rr = pos2row[i];
-        // first position j < i with P[rr] bit j
-        uint64_t word = 0ull;
-        if (lane < (uint32_t)W) {
-          word = P[rr * W + lane];
-          const uint32_t lo = lane * 64u;
-          if (lo >= i) word = 0ull;
-          else if (i - lo < 64u) word &= (1ull << (i - lo)) - 1ull;
-        }
-        const uint64_t nz = __ballot(word != 0ull);
-        const uint32_t wd = (uint32_t)(__ffsll((unsigned long long)nz) - 1);
-        const uint64_t wbits = shfl64(word, wd);
-        const uint32_t j = wd * 64u + (uint32_t)(__ffsll((unsigned long long)wbits) - 1);
-        const uint32_t c = pos2row[j];
-        const uint32_t ca = cnt[rr], cb = cnt[c];
-        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
-        float* xc = r.x + (size_t)slot[c] * r.dp;
-        float* rowc = ROWS_LDS ? rows + c * ST : xc;
-        const float* rowr = row_ptr(rr);
-        for (int k = (int)lane; k < D; k += 64) {
-          const float v = consensus(rowr[k], fa, rowc[k], fb, fn);
-          if (ROWS_LDS) rowc[k] = v;
-          xc[k] = v;
-        }
-        lds_fence();  // workgroup-scope fence: LDS and global stores of this wave
-        if (lane == 0) {
-          float nn = 0.0f;
-          for (int k = 0; k < D; ++k) nn = nn + rowc[k] * rowc[k];
-          nrm[c] = nn;
-          sq[c] = __builtin_sqrtf(nn);
-          r.nxt[tl[rr]] = hd[c];  // ids_current ++ ids_candidate
-          hd[c] = hd[rr];
-          cnt[c] = ca + cb;
-          cnt[rr] = 0u;
-          pos2row[i] = pos2row[size - 1];  // swap-remove
-        }
-        lds_fence();
-        --size;
-        const float sc = sq[c];
-        const uint32_t moved = size;  // old position of the row now at i
-        for (uint32_t qq = i + lane; qq < size; qq += 64) {  // rows still to be visited
-          const uint32_t y = pos2row[qq];
-          uint64_t* Py = P + y * W;
-          // the row that sat at position `moved` is now at position i
-          const bool bm = (Py[moved / 64] >> (moved & 63u)) & 1ull;
-          Py[moved / 64] &= ~(1ull << (moved & 63u));
-          Py[i / 64] = bm ? (Py[i / 64] | (1ull << (i & 63u))) : (Py[i / 64] & ~(1ull << (i & 63u)));
-          float dot;
-          if constexpr (ROWS_LDS) dot = dot_lds_lds<D>(row_ptr(y), rowc);
-          else dot = dot_mem_mem(row_ptr(y), rowc, D);
-          const bool dn = decide(dc, dot, sq[y] * sc);
-          Py[j / 64] = dn ? (Py[j / 64] | (1ull << (j & 63u))) : (Py[j / 64] & ~(1ull << (j & 63u)));
-        }
-        lds_fence();
-      }
-      // write back
-      for (uint32_t q = lane; q < b; q += 64) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
-      for (uint32_t q0 = 0; q0 < size; q0 += 64) {  // uniform trip count (ballot inside)
-        const uint32_t q = q0 + lane;
-        bool rewritten = false;
-        if (q < size) {
-          const uint32_t y = pos2row[q];
-          rewritten = r.cnt[slot[y]] != cnt[y];  // every merge into a row raises its count
-          r.nrm[slot[y]] = nrm[y];
-          r.cnt[slot[y]] = cnt[y];
-          r.head[slot[y]] = hd[y];
-        }
-        if (dlist) append_slot(rewritten, q < size ? slot[pos2row[q]] : 0u, dlist, &ctr->n_delta);
-      }
-    }
+    big_walk<RB, NT>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq, ROWS_LDS ? rows : nullptr, ST,
+                     rows, wbuf, r, dc, slots, dlist, ctr);
     __syncthreads();
   }
 }
@@ -697,21 +754,6 @@ __device__ __forceinline__ void stage_chunk(const float* __restrict__ X, int dp,
 #pragma unroll
   for (int it = 0; it < 16; ++it)
     if (col_ok) *reinterpret_cast<float4*>(tile + (it * 4 + rsub) * ST + 4 * q) = v[it];
-}
-
-// s + sequential sum of a[e] * b[e], e < n, a and b in memory (16-B aligned rows)
-__device__ __forceinline__ float dot_acc_mem(float s, const float* a, const float* b, int n) {
-  int k = 0;
-  for (; k + 4 <= n; k += 4) {
-    const float4 u = *reinterpret_cast<const float4*>(a + k);
-    const float4 v = *reinterpret_cast<const float4*>(b + k);
-    s = s + u.x * v.x;
-    s = s + u.y * v.y;
-    s = s + u.z * v.z;
-    s = s + u.w * v.w;
-  }
-  for (; k < n; ++k) s = s + a[k] * b[k];
-  return s;
 }
 
 template <int N>
@@ -907,6 +949,7 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__
   uint32_t* tl = slot + 4 * RB;
   uint32_t* pos2row = slot + 5 * RB;
   float* sq = reinterpret_cast<float*>(slot + 6 * RB);
+  __shared__ uint32_t wbuf[2 * NW];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   float* ctile = reinterpret_cast<float*>(smem + L::tiles) + wv * 64 * STB;  // this wave's
   const int d = r.d, dp = r.dp;
@@ -991,92 +1034,8 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__
     }
     __syncthreads();
 
-    // the walk, by wave 0 (as k_merge_big with rows in memory)
-    if (wv == 0) {
-      uint32_t i = 1, size = b;
-      while (true) {
-        uint32_t q = size;
-        for (uint32_t q0 = i; q0 < size; q0 += 64) {
-          const uint32_t qq = q0 + lane;
-          bool hit = false;
-          if (qq < size) {
-            const uint64_t* Py = P + pos2row[qq] * W;
-#pragma unroll
-            for (int k = 0; k < W; ++k) {
-              const uint32_t lo = (uint32_t)k * 64u;
-              if (lo < qq) {
-                const uint64_t wk = Py[k];
-                hit |= (qq - lo >= 64u ? wk : (wk & ((1ull << (qq - lo)) - 1ull))) != 0ull;
-              }
-            }
-          }
-          const uint64_t m = __ballot(hit);
-          if (m != 0ull) {
-            q = q0 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
-            break;
-          }
-        }
-        if (q >= size) break;
-        i = q;
-        const uint32_t rr = pos2row[i];
-        uint64_t word = 0ull;
-        if (lane < (uint32_t)W) {
-          word = P[rr * W + lane];
-          const uint32_t lo = lane * 64u;
-          if (lo >= i) word = 0ull;
-          else if (i - lo < 64u) word &= (1ull << (i - lo)) - 1ull;
-        }
-        const uint64_t nz = __ballot(word != 0ull);
-        const uint32_t wd = (uint32_t)(__ffsll((unsigned long long)nz) - 1);
-        const uint64_t wbits = shfl64(word, wd);
-        const uint32_t j = wd * 64u + (uint32_t)(__ffsll((unsigned long long)wbits) - 1);
-        const uint32_t c = pos2row[j];
-        const uint32_t ca = cnt[rr], cb = cnt[c];
-        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
-        float* xc = r.x + (size_t)slot[c] * dp;
-        const float* xr = row_ptr(rr);
-        for (int k = (int)lane; k < d; k += 64) xc[k] = consensus(xr[k], fa, xc[k], fb, fn);
-        lds_fence();
-        if (lane == 0) {
-          const float nn = dot_acc_mem(0.0f, xc, xc, d);
-          nrm[c] = nn;
-          sq[c] = __builtin_sqrtf(nn);
-          r.nxt[tl[rr]] = hd[c];  // ids_current ++ ids_candidate
-          hd[c] = hd[rr];
-          cnt[c] = ca + cb;
-          cnt[rr] = 0u;
-          pos2row[i] = pos2row[size - 1];  // swap-remove
-        }
-        lds_fence();
-        --size;
-        const float sc = sq[c];
-        const uint32_t moved = size;
-        for (uint32_t qq = i + lane; qq < size; qq += 64) {
-          const uint32_t y = pos2row[qq];
-          uint64_t* Py = P + y * W;
-          const bool bm = (Py[moved / 64] >> (moved & 63u)) & 1ull;
-          Py[moved / 64] &= ~(1ull << (moved & 63u));
-          Py[i / 64] = bm ? (Py[i / 64] | (1ull << (i & 63u))) : (Py[i / 64] & ~(1ull << (i & 63u)));
-          const float dot = dot_acc_mem(0.0f, row_ptr(y), xc, d);
-          const bool dn = decide(dc, dot, sq[y] * sc);
-          Py[j / 64] = dn ? (Py[j / 64] | (1ull << (j & 63u))) : (Py[j / 64] & ~(1ull << (j & 63u)));
-        }
-        lds_fence();
-      }
-      for (uint32_t q = lane; q < b; q += 64) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
-      for (uint32_t q0 = 0; q0 < size; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        bool rewritten = false;
-        if (q < size) {
-          const uint32_t y = pos2row[q];
-          rewritten = r.cnt[slot[y]] != cnt[y];
-          r.nrm[slot[y]] = nrm[y];
-          r.cnt[slot[y]] = cnt[y];
-          r.head[slot[y]] = hd[y];
-        }
-        if (dlist) append_slot(rewritten, q < size ? slot[pos2row[q]] : 0u, dlist, &ctr->n_delta);
-      }
-    }
+    big_walk<RB, NT>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq, nullptr, 0,
+                     reinterpret_cast<float*>(smem + L::tiles), wbuf, r, dc, slots, dlist, ctr);
     __syncthreads();
   }
 }
@@ -1135,6 +1094,32 @@ static void launch_big(const MergeWork& w, int c, uint32_t* slots, const Decider
   k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist);
 }
 
+// Fork the size-class kernels onto the auxiliary streams (after k_classify on s) and join them
+// back into s.  Every class writes disjoint runs, so the order between classes is free.
+struct Fork {
+  const MergeWork& w;
+  hipStream_t s;
+  bool on;
+  Fork(const MergeWork& w_, hipStream_t s_) : w(w_), s(s_) {
+    static const bool enabled = [] {
+      const char* e = getenv("KLSH_MERGE_STREAMS");
+      return !(e && e[0] == '0');
+    }();
+    on = enabled && w.aux[0] != nullptr;
+    if (!on) return;
+    (void)hipEventRecord(w.fork, s);
+    for (int i = 0; i < kMergeStreams; ++i) (void)hipStreamWaitEvent(w.aux[i], w.fork, 0);
+  }
+  hipStream_t lane(int i) const { return on ? w.aux[i] : s; }
+  ~Fork() {
+    if (!on) return;
+    for (int i = 0; i < kMergeStreams; ++i) {
+      (void)hipEventRecord(w.join[i], w.aux[i]);
+      (void)hipStreamWaitEvent(s, w.join[i], 0);
+    }
+  }
+};
+
 template <int D>
 static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
                           uint32_t* slots, const Decider& dc, const MergeWork& w, Counters* ctr,
@@ -1144,17 +1129,20 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   auto grid = [&](int c, uint32_t per_wave) {
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
-  k_merge_group<2, D><<<grid(0, 32), 64, 0, s>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
-  k_merge_group<4, D><<<grid(1, 16), 64, 0, s>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
-  k_merge_group<8, D><<<grid(2, 8), 64, 0, s>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
-  k_merge_group<16, D><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
-  k_merge_group<32, D><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
-  k_merge_group<64, D><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
-  launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, s);
-  launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, s);
-  launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, s);
+  const Fork f(w, s);
   const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 1] + 1) + 1);
-  k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
+  // longest walks first on each stream
+  launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(0));
+  launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, f.lane(0));
+  k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, f.lane(0)>>>(w.huge, &ctr->n_huge, slots, dc, r,
+                                                               w, ctr);
+  launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
+  k_merge_group<64, D><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
+  k_merge_group<32, D><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
+  k_merge_group<16, D><<<grid(3, 4), 64, 0, f.lane(2)>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
+  k_merge_group<8, D><<<grid(2, 8), 64, 0, f.lane(2)>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
+  k_merge_group<4, D><<<grid(1, 16), 64, 0, f.lane(2)>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
+  k_merge_group<2, D><<<grid(0, 32), 64, 0, f.lane(2)>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
 }
 
 template <int RB, int NT, int KC>
@@ -1179,17 +1167,19 @@ static void launch_groups_wide(const Rows& r, const uint32_t* seg, uint32_t hi, 
   auto grid = [&](int c, uint32_t per_wave) {
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
-  k_merge_group_wide<2><<<grid(0, 32), 64, 0, s>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<4><<<grid(1, 16), 64, 0, s>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<8><<<grid(2, 8), 64, 0, s>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<16><<<grid(3, 4), 64, 0, s>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<32><<<grid(4, 2), 64, 0, s>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<64><<<grid(5, 1), 64, 0, s>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
-  launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, s);
-  launch_big_wide<384, 256, 32>(w, 1, slots, dc, r, ctr, n, s);
-  launch_big_wide<896, 256, 16>(w, 2, slots, dc, r, ctr, n, s);
+  const Fork f(w, s);
   const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 1] + 1) + 1);
-  k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
+  launch_big_wide<384, 256, 32>(w, 1, slots, dc, r, ctr, n, f.lane(0));
+  launch_big_wide<896, 256, 16>(w, 2, slots, dc, r, ctr, n, f.lane(0));
+  k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, f.lane(0)>>>(w.huge, &ctr->n_huge, slots, dc, r,
+                                                               w, ctr);
+  launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, f.lane(1));
+  k_merge_group_wide<64><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<32><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<16><<<grid(3, 4), 64, 0, f.lane(2)>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<8><<<grid(2, 8), 64, 0, f.lane(2)>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<4><<<grid(1, 16), 64, 0, f.lane(2)>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
+  k_merge_group_wide<2><<<grid(0, 32), 64, 0, f.lane(2)>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
 }
 
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
