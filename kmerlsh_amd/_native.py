@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libklsh.so")
+# KLSH_LIB overrides the library path (A/B runs of engine builds; the default is the in-tree build)
+LIB_PATH = os.environ.get("KLSH_LIB") or os.path.join(_HERE, "lib", "libklsh.so")
 CLI_PATH = os.path.join(_HERE, "bin", "kmerLSH")
 
 KLSH_OK = 0

@@ -81,6 +81,34 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ X, int dp, 
     *reinterpret_cast<float4*>(tile + (it * RPI + rsub) * (D + 4) + 4 * q) = v[it];
 }
 
+// stage_rows split in two, so a wave can issue the next batch's row loads early (software
+// pipelining) and store them to LDS later: gather_rows loads this wave's 64 rows into v[],
+// store_rows writes v[] to the tile (the same layout as stage_rows).
+template <int D>
+__device__ __forceinline__ void gather_rows(const float* __restrict__ X, int dp, uint32_t slot,
+                                            bool valid, float4 (&v)[D / 4]) {
+  constexpr int CPR = D / 4, RPI = 64 / CPR;
+  const uint32_t lane = __lane_id();
+  const uint32_t q = lane % CPR, rsub = lane / CPR;
+#pragma unroll
+  for (int it = 0; it < CPR; ++it) {
+    const uint32_t row = it * RPI + rsub;
+    const uint32_t s = (uint32_t)__shfl((int)slot, (int)row, 64);
+    const int ok = __shfl(valid ? 1 : 0, (int)row, 64);
+    v[it] = ok ? *reinterpret_cast<const float4*>(X + (size_t)s * dp + 4 * q)
+               : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+template <int D>
+__device__ __forceinline__ void store_rows(const float4 (&v)[D / 4], float* tile) {
+  constexpr int CPR = D / 4, RPI = 64 / CPR;
+  const uint32_t lane = __lane_id();
+  const uint32_t q = lane % CPR, rsub = lane / CPR;
+#pragma unroll
+  for (int it = 0; it < CPR; ++it)
+    *reinterpret_cast<float4*>(tile + (it * RPI + rsub) * (D + 4) + 4 * q) = v[it];
+}
+
 __device__ __forceinline__ float dot_mem_mem(const float* a, const float* b, int d) {
   float s = 0.0f;
   for (int k = 0; k < d; ++k) s = s + a[k] * b[k];

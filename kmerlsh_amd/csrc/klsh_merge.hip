@@ -33,9 +33,22 @@ namespace klsh {
 
 // ------------------------------------------------------------------------------- helpers -----
 __device__ __forceinline__ void lds_fence() {
-  // orders this workgroup's LDS stores before later LDS loads from other lanes of the same wave
-  // (LDS executes one wave's instructions in order) and stops the compiler moving memory ops
+  // orders this workgroup's LDS and global stores before later loads from other lanes of the same
+  // wave (waits for outstanding global stores: use only where a global store must be seen)
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+__device__ __forceinline__ void wave_lds_fence() {
+  // LDS executes one wave's instructions in order: within a wave only the compiler must be kept
+  // from moving LDS accesses across this point (no wait for outstanding global stores)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+__device__ __forceinline__ void lds_barrier() {
+  // workgroup barrier for LDS data only: this wave's LDS stores have landed (lgkmcnt(0)), then
+  // s_barrier — without the vmcnt(0) wait of __syncthreads for outstanding global stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
@@ -163,8 +176,15 @@ __device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucke
 // g of its run and owns row id g: row in registers x[] and at LDS row `lane`.
 // One batch: run (p, b) of lane's group, lane's slot already loaded (the caller pipelines those
 // loads one batch ahead, so only the row gather is exposed here).
-template <int G, int D>
+#ifndef KLSH_ROW_PREFETCH
+#define KLSH_ROW_PREFETCH 0
+#endif
+constexpr bool kRowPrefetch = KLSH_ROW_PREFETCH != 0;
+
+template <int G, int D, class Prefetch>
 __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
+                                            float4 (&rb)[kRowPrefetch ? D / 4 : 1],
+                                            Prefetch prefetch,
                                             uint32_t* slots, const Decider& dc, const Rows& r,
                                             float* lds, uint32_t* dlist, Counters* ctr) {
   constexpr int ST = D + 4;  // padded row stride: 16 lanes of a ds_read_b128 hit distinct banks
@@ -179,9 +199,14 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
     uint32_t cnt = valid ? r.cnt[slot] : 0u;
     uint32_t hd = valid ? r.head[slot] : 0u;
     const uint32_t tl = valid ? r.tail[slot] : 0u;
-    stage_rows<D>(r.x, r.dp, slot, valid, lds);  // row of lane l -> LDS row l, coalesced
-    float sq = __builtin_sqrtf(nrm);             // this row's sqrtf(|x|^2), distance.cc:37
-    lds_fence();
+    if constexpr (kRowPrefetch) {
+      store_rows<D>(rb, lds);  // rows gathered one batch ahead -> LDS row l = lane l's row
+    } else {
+      stage_rows<D>(r.x, r.dp, slot, valid, lds);  // row of lane l -> LDS row l, coalesced
+    }
+    float sq = __builtin_sqrtf(nrm);  // this row's sqrtf(|x|^2), distance.cc:37
+    if constexpr (kRowPrefetch) prefetch();  // the next batch's row loads fly during this batch
+    wave_lds_fence();
     float x[D];
     load_row<D>(myrow, x);
     const uint32_t bmax = wave_max(b);
@@ -250,13 +275,10 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
         const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
         const float* rowr = lds + (gbase + rr) * ST;
         float* rowc = lds + (gbase + c) * ST;
-        float* xc = r.x + (size_t)slot_c * r.dp;
-        for (int k = (int)g; k < D; k += G) {  // consensus, split over the group's lanes
-          const float v = consensus(rowr[k], fa, rowc[k], fb, fn);
-          rowc[k] = v;
-          xc[k] = v;
-        }
-        lds_fence();
+        (void)slot_c;
+        for (int k = (int)g; k < D; k += G)  // consensus, split over the group's lanes (LDS only:
+          rowc[k] = consensus(rowr[k], fa, rowc[k], fb, fn);  // rewritten rows go out at the end)
+        wave_lds_fence();
         // one pass: lane c (the new row c, reloaded) gets its exact sequential norm
         // (distance.cc:33-34), every other lane the dot product of its row with row c
         if (g == c) load_row<D>(rowc, x);
@@ -281,17 +303,21 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
       }
     }
 
-    // 3. write back: survivors in position order, kInvalid after; changed rows' metadata
+    // 3. write back: survivors in position order, kInvalid after; changed rows and metadata
     const uint32_t pos_slot = shfl32(slot, gbase + rowid);
     if (valid) slots[p + g] = g < size ? pos_slot : kInvalid;
     if (valid && alive && dirty) {
+      float* xo = r.x + (size_t)slot * r.dp;
+#pragma unroll
+      for (int k = 0; k < D; k += 4)
+        *reinterpret_cast<float4*>(xo + k) = *reinterpret_cast<const float4*>(myrow + k);
       r.nrm[slot] = nrm;
       r.cnt[slot] = cnt;
       r.head[slot] = hd;
     }
     if (dlist) append_slot(valid && alive && dirty, slot, dlist, &ctr->n_delta);
     if (valid && !alive) r.cnt[slot] = 0u;
-    lds_fence();
+    wave_lds_fence();
   }
 }
 
@@ -354,14 +380,72 @@ __global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ li
   };
   uint2 e = entry(blockIdx.x);
   uint32_t slot = g < e.y ? slots[e.x + g] : 0u;
+  float4 rb[kRowPrefetch ? D / 4 : 1];  // this wave's 64 rows, loaded one batch ahead
+  if constexpr (kRowPrefetch) gather_rows<D>(r.x, r.dp, slot, g < e.y, rb);
   uint2 e_next = entry(blockIdx.x + gridDim.x);
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
     const uint32_t slot_next = g < e_next.y ? slots[e_next.x + g] : 0u;
     const uint2 e_next2 = entry(bi + 2 * gridDim.x);
-    merge_batch<G, D>(e.x, e.y, slot, slots, dc, r, lds, dlist, ctr);
+    merge_batch<G, D>(e.x, e.y, slot, rb,
+                      [&] {
+                        if constexpr (kRowPrefetch)
+                          gather_rows<D>(r.x, r.dp, slot_next, g < e_next.y, rb);
+                      },
+                      slots, dc, r, lds, dlist, ctr);
     e = e_next;
     slot = slot_next;
     e_next = e_next2;
+  }
+}
+
+// Runs of exactly 2 rows (the commonest run): p_cluster visits i = 1 once — if row 1 matches
+// row 0, row 0 becomes SetConsensus(row 1, row 0) and row 1 dies.  One lane per run, both rows in
+// registers, no LDS and no cross-lane traffic.
+template <int D>
+__global__ __launch_bounds__(256) void k_merge_pair(const uint2* __restrict__ list, int cls,
+                                                   uint32_t* __restrict__ slots, Decider dc,
+                                                   Rows r, Counters* ctr, uint32_t* dlist) {
+  const uint32_t n = __hip_atomic_load(&ctr->n_cls[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t k0 = blockIdx.x * 256u; k0 < n; k0 += gridDim.x * 256u) {  // uniform per block
+    const uint32_t k = k0 + threadIdx.x;
+    bool merged = false;
+    uint32_t s0 = 0;
+    if (k < n) {
+      const uint2 e = list[k];
+      s0 = slots[e.x];
+      const uint32_t s1 = slots[e.x + 1];
+      float x0[D], x1[D];
+      load_row<D>(r.x + (size_t)s0 * r.dp, x0);
+      load_row<D>(r.x + (size_t)s1 * r.dp, x1);
+      float dot = 0.0f;
+#pragma unroll
+      for (int q = 0; q < D; ++q) dot = dot + x1[q] * x0[q];  // cosine(c[1], c[0]), in order
+      const float n0 = r.nrm[s0], n1 = r.nrm[s1];
+      if (decide(dc, dot, __builtin_sqrtf(n1) * __builtin_sqrtf(n0))) {
+        merged = true;
+        const uint32_t ca = r.cnt[s1], cb = r.cnt[s0];  // current = row 1, candidate = row 0
+        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+        float nn = 0.0f;
+        float* xo = r.x + (size_t)s0 * r.dp;
+#pragma unroll
+        for (int q = 0; q < D; q += 4) {
+          float4 v;
+          v.x = consensus(x1[q], fa, x0[q], fb, fn);
+          v.y = consensus(x1[q + 1], fa, x0[q + 1], fb, fn);
+          v.z = consensus(x1[q + 2], fa, x0[q + 2], fb, fn);
+          v.w = consensus(x1[q + 3], fa, x0[q + 3], fb, fn);
+          nn = nn + v.x * v.x;
+          nn = nn + v.y * v.y;
+          nn = nn + v.z * v.z;
+          nn = nn + v.w * v.w;
+          *reinterpret_cast<float4*>(xo + q) = v;
+        }
+        r.nrm[s0] = nn;
+        link_members(r, s1, s0);  // ids_current ++ ids_candidate; cnt[s1] = 0
+        slots[e.x + 1] = kInvalid;
+      }
+    }
+    if (dlist) append_slot(merged, s0, dlist, &ctr->n_delta);
   }
 }
 
@@ -392,7 +476,7 @@ __device__ __forceinline__ float dot_acc_mem(float s, const float* a, const floa
 // there, and recomputes the decisions of the rows still to be visited against the new row —
 // spread over all NT lanes (the new row's norm on one lane meanwhile).  Rows are read from
 // rowsL (LDS, stride ST) if given, else from memory; the new row is kept in LDS (cbuf).
-template <int RB, int NT>
+template <int RB, int NT, bool ROWS_LDS>
 __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, uint32_t* slot,
                                          float* nrm, uint32_t* cnt, uint32_t* hd, uint32_t* tl,
                                          uint32_t* pos2row, float* sq, float* rowsL, int ST,
@@ -403,7 +487,7 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const int d = r.d, dp = r.dp;
   auto rowp = [&](uint32_t a) -> const float* {
-    return rowsL ? rowsL + a * ST : r.x + (size_t)slot[a] * dp;
+    return ROWS_LDS ? rowsL + a * ST : r.x + (size_t)slot[a] * dp;
   };
   uint32_t i = 1, size = b, par = 0;
   while (true) {
@@ -427,7 +511,7 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
       if (lane == 0)
         wbuf[par * NW + wv] = m ? q0 + wv * 64u + (uint32_t)(__ffsll((unsigned long long)m) - 1)
                                 : 0xFFFFFFFFu;
-      __syncthreads();
+      lds_barrier();
       uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
       for (int w = 0; w < NW; ++w) best = min(best, wbuf[par * NW + w]);
@@ -456,16 +540,16 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
     const uint32_t ca = cnt[rr], cb = cnt[c];
     const uint32_t hr = hd[rr], tr = tl[rr], hc = hd[c];
     const uint32_t moved_row = pos2row[size - 1];
-    __syncthreads();  // all reads of the old state are done
+    lds_barrier();  // all reads of the old state are done
     // 3. consensus (funcAB.cc:65), current row first; member links and the swap-remove
     const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
     float* xc = r.x + (size_t)slot[c] * dp;
     const float* xr = rowp(rr);
-    float* lc = rowsL ? rowsL + c * ST : cbuf;  // the new row c, in LDS
+    float* lc = ROWS_LDS ? rowsL + c * ST : cbuf;  // the new row c, in LDS
     for (int k = (int)t; k < d; k += NT) {
-      const float v = consensus(xr[k], fa, rowsL ? lc[k] : xc[k], fb, fn);
+      const float v = consensus(xr[k], fa, ROWS_LDS ? lc[k] : xc[k], fb, fn);
       lc[k] = v;
-      xc[k] = v;
+      if (!ROWS_LDS) xc[k] = v;  // rows in LDS go out once, at the end of the run
     }
     if (t == 0) {
       r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
@@ -474,7 +558,8 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
       cnt[rr] = 0u;
       pos2row[i] = moved_row;
     }
-    __syncthreads();
+    if (ROWS_LDS) lds_barrier();
+    else __syncthreads();  // the new row in memory is visible to the workgroup
     --size;
     const uint32_t moved = size;  // old position of the row now at i
     // 4. dot products of the rows still to be visited with row c; row c's norm
@@ -489,7 +574,7 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
       nrm[c] = nn;
       sq[c] = __builtin_sqrtf(nn);
     }
-    __syncthreads();
+    lds_barrier();
     // 5. position-space bits: the moved row's bit goes to position i, bit j is re-decided
     const float sc = sq[c];
 #pragma unroll
@@ -505,10 +590,21 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
         Py[j / 64] = dn ? (Py[j / 64] | (1ull << (j & 63u))) : (Py[j / 64] & ~(1ull << (j & 63u)));
       }
     }
+    lds_barrier();
+  }
+  // write back: survivors in position order, kInvalid after; rewritten rows; metadata
+  for (uint32_t q = t; q < b; q += NT) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
+  if (ROWS_LDS) {  // a survivor was rewritten iff its count rose (the global count is still old)
+    const uint32_t c4 = (uint32_t)dp / 4;
+    for (uint32_t idx = t; idx < size * c4; idx += NT) {
+      const uint32_t q = idx / c4, k = (idx % c4) * 4;
+      const uint32_t y = pos2row[q];
+      if (r.cnt[slot[y]] != cnt[y])
+        *reinterpret_cast<float4*>(r.x + (size_t)slot[y] * dp + k) =
+            *reinterpret_cast<const float4*>(rowsL + y * ST + k);
+    }
     __syncthreads();
   }
-  // write back: survivors in position order, kInvalid after; metadata of the survivors
-  for (uint32_t q = t; q < b; q += NT) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
   for (uint32_t q0 = 0; q0 < size; q0 += NT) {  // uniform trip count (ballot inside)
     const uint32_t q = q0 + t;
     bool rewritten = false;
@@ -636,8 +732,8 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
     }
     __syncthreads();
 
-    big_walk<RB, NT>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq, ROWS_LDS ? rows : nullptr, ST,
-                     rows, wbuf, r, dc, slots, dlist, ctr);
+    big_walk<RB, NT, ROWS_LDS>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq,
+                               ROWS_LDS ? rows : nullptr, ST, rows, wbuf, r, dc, slots, dlist, ctr);
     __syncthreads();
   }
 }
@@ -801,9 +897,9 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
   for (int k = 0; k < NK; ++k) acc[k] = 0.0f;
   for (int c0 = 0; c0 < d; c0 += kWideKC) {
     const int n = min(kWideKC, d - c0), kcp = min(kWideKC, dp - c0);
-    lds_fence();  // the previous chunk's reads are done
+    wave_lds_fence();  // the previous chunk's reads are done
     stage_chunk(r.x, dp, slot, valid, c0, kcp, tile);
-    lds_fence();
+    wave_lds_fence();
     const float* mine = tile + lane * ST;
     if (n == kWideKC) {
       float x[kWideKC];
@@ -1034,7 +1130,7 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__
     }
     __syncthreads();
 
-    big_walk<RB, NT>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq, nullptr, 0,
+    big_walk<RB, NT, false>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq, nullptr, 0,
                      reinterpret_cast<float*>(smem + L::tiles), wbuf, r, dc, slots, dlist, ctr);
     __syncthreads();
   }
@@ -1120,6 +1216,10 @@ struct Fork {
   }
 };
 
+static uint32_t pair_grid(uint32_t n) {  // one lane per run of 2: at most n / 2 runs
+  return (uint32_t)std::min<uint64_t>(4096, (n / 2 + 255) / 256 + 1);
+}
+
 template <int D>
 static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
                           uint32_t* slots, const Decider& dc, const MergeWork& w, Counters* ctr,
@@ -1142,7 +1242,7 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   k_merge_group<16, D><<<grid(3, 4), 64, 0, f.lane(2)>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
   k_merge_group<8, D><<<grid(2, 8), 64, 0, f.lane(2)>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
   k_merge_group<4, D><<<grid(1, 16), 64, 0, f.lane(2)>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
-  k_merge_group<2, D><<<grid(0, 32), 64, 0, f.lane(2)>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
+  k_merge_pair<D><<<pair_grid(n), 256, 0, f.lane(2)>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
 }
 
 template <int RB, int NT, int KC>
