@@ -15,7 +15,7 @@ constexpr int kScanTile = 4096;             // items per scan workgroup (256 lan
 
 // Bucket runs of 65..896 rows are merged by one workgroup with the run's decision matrix in LDS
 // (k_merge_big; three size classes, rows in LDS up to 384); longer runs by one wave from memory
-// (k_merge_wave).
+// (k_merge_huge).
 constexpr int kBigClasses = 3;
 constexpr int kBigRows[kBigClasses] = {128, 384, 896};
 
@@ -29,7 +29,7 @@ struct Counters {
   uint32_t n_seg;                  // bucket runs found by the segment scan
   uint32_t n_cls[kGroupClasses];   // runs of 2..64 rows queued per size class
   uint32_t n_big[kBigClasses];     // runs of 65..896 rows queued for k_merge_big, per class
-  uint32_t n_huge;                 // longer runs queued for k_merge_wave
+  uint32_t n_huge;                 // longer runs queued for k_merge_huge
   uint32_t n_over;                 // runs longer than bucket_size_threshold (nestedCluster)
   uint32_t total;                  // result of the last scan/compaction (live rows)
   uint32_t n_delta;                // sharded loop: survivors rewritten by a merge this iteration
@@ -41,7 +41,7 @@ struct MergeWork {
   uint32_t* seg;                   // run starts [n_seg]
   uint2* cls[kGroupClasses];       // (start, length) of runs per size class
   uint2* big[kBigClasses];         // (start, length) of runs for k_merge_big, per class
-  uint2* huge;                     // (start, length) of runs for k_merge_wave
+  uint2* huge;                     // (start, length) of runs for k_merge_huge
   uint2* over;                     // (start, length) of oversize runs
   uint32_t* tile_sums;
   // Sharded loop only (nullptr otherwise): every survivor a merge rewrote is appended to dlist

@@ -19,7 +19,7 @@
 //   k_merge_big     one workgroup per run of 65..896 rows: the same scheme with the run's
 //                   decision matrix (and rows, up to 384) in LDS, kept in POSITION space so
 //                   every step of the walk is a few bit operations.
-//   k_merge_wave    longer runs: one wave per run, the reference order directly.
+//   k_merge_huge    longer runs: one workgroup per run, the reference order directly.
 //
 // Results are positional (survivors in place, kInvalid after), so they do not depend on which
 // wave handled which run or in what order.
@@ -738,89 +738,115 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
   }
 }
 
-// ---------------------------------------------------------------- runs longer than that -----
-// One wave per run, the reference order directly: for the visited row i the lanes test
-// candidates j = c*64 + lane, the lowest lane of the first chunk with a hit is the first match.
-template <int D>
-__global__ __launch_bounds__(64) void k_merge_wave(const uint2* __restrict__ list,
-                                                   const uint32_t* count_ptr,
-                                                   uint32_t* __restrict__ slots, Decider dc,
-                                                   Rows r, MergeWork w, Counters* ctr) {
-  extern __shared__ __attribute__((aligned(16))) float sx[];  // consensus row for the norm
-  const uint32_t lane = threadIdx.x;
+// ------------------------------------------------------ runs longer than 896 rows: workgroups -----
+// The reference walk directly (no decision matrix: it would not fit), one workgroup of NT lanes
+// per run: the visited row i sits in LDS, every lane tests one candidate j < i per chunk (rows
+// from memory, one exact sequential dot product each), and the first hit of the chunk is found
+// by a ballot + cross-wave min.  The run's slots and sqrtf(norms) live in LDS when they fit.
+constexpr int kHugeNT = 512;
+constexpr uint32_t kHugeLdsRows = 8192;
+
+__global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict__ list,
+                                                       const uint32_t* count_ptr,
+                                                       uint32_t* __restrict__ slots, Decider dc,
+                                                       Rows r, MergeWork w, Counters* ctr) {
+  constexpr int NW = kHugeNT / 64;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* ls = reinterpret_cast<uint32_t*>(smem);             // [kHugeLdsRows] slots
+  float* lq = reinterpret_cast<float*>(ls + kHugeLdsRows);       // [kHugeLdsRows] sqrtf(nrm)
+  float* xi = lq + kHugeLdsRows;                                 // [dp] the visited row
+  __shared__ uint32_t wmin[2][NW];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const int d = r.d, dp = r.dp;
   const uint32_t count = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int d = r.d;
+  uint32_t par = 0;
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
     const uint2 e = list[li];
     const uint32_t p = e.x, b = e.y;
-    uint32_t* s = slots + p;
+    const bool in_lds = b <= kHugeLdsRows;
+    uint32_t* S = in_lds ? ls : slots + p;
+    if (in_lds)
+      for (uint32_t a = t; a < b; a += kHugeNT) {
+        const uint32_t sa = slots[p + a];
+        ls[a] = sa;
+        lq[a] = __builtin_sqrtf(r.nrm[sa]);
+      }
+    __syncthreads();
+    auto sqrt_at = [&](uint32_t a) { return in_lds ? lq[a] : __builtin_sqrtf(r.nrm[S[a]]); };
     uint32_t size = b, i = 1;
-    while (i < size) {
-      const uint32_t si = s[i];
-      const float* xip = r.x + (size_t)si * r.dp;
-      const float sqi = __builtin_sqrtf(r.nrm[si]);
-      int found = -1;
-      if constexpr (D > 0) {
-        float xi[D > 0 ? D : 4];
-        load_row<(D > 0 ? D : 4)>(xip, xi);
-        for (uint32_t c = 0; c < i; c += 64) {
-          const uint32_t j = c + lane;
-          bool ok = false;
-          if (j < i) {
-            const uint32_t sj = s[j];
-            ok = decide(dc, dot_reg_mem<(D > 0 ? D : 4)>(xi, r.x + (size_t)sj * r.dp),
-                        sqi * __builtin_sqrtf(r.nrm[sj]));
-          }
-          const uint64_t m = __ballot(ok);
-          if (m) {
-            found = (int)(c + (uint32_t)(__ffsll((unsigned long long)m) - 1));
-            break;
-          }
+    while (i < size) {  // block-uniform
+      const uint32_t si = S[i];
+      const float sqi = sqrt_at(i);
+      for (int k = (int)t * 4; k < dp; k += kHugeNT * 4)
+        *reinterpret_cast<float4*>(xi + k) =
+            *reinterpret_cast<const float4*>(r.x + (size_t)si * dp + k);
+      __syncthreads();
+      uint32_t found = 0xFFFFFFFFu;
+      for (uint32_t c0 = 0; c0 < i; c0 += kHugeNT) {  // the first j < i that matches
+        const uint32_t j = c0 + t;
+        bool ok = false;
+        if (j < i) {
+          const uint32_t sj = S[j];
+          ok = decide(dc, dot_acc_mem(0.0f, xi, r.x + (size_t)sj * dp, d), sqi * sqrt_at(j));
         }
-      } else {
-        for (uint32_t c = 0; c < i; c += 64) {
-          const uint32_t j = c + lane;
-          bool ok = false;
-          if (j < i) {
-            const uint32_t sj = s[j];
-            ok = decide(dc, dot_mem_mem(xip, r.x + (size_t)sj * r.dp, d),
-                        sqi * __builtin_sqrtf(r.nrm[sj]));
-          }
-          const uint64_t m = __ballot(ok);
-          if (m) {
-            found = (int)(c + (uint32_t)(__ffsll((unsigned long long)m) - 1));
-            break;
-          }
+        const uint64_t m = __ballot(ok);
+        if (lane == 0)
+          wmin[par][wv] = m ? c0 + wv * 64u + (uint32_t)(__ffsll((unsigned long long)m) - 1)
+                            : 0xFFFFFFFFu;
+        __syncthreads();
+        uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) best = min(best, wmin[par][q]);
+        par ^= 1u;
+        if (best != 0xFFFFFFFFu) {  // block-uniform
+          found = best;
+          break;
         }
       }
-      if (found >= 0) {
-        const uint32_t sj = s[found];
-        float* xj = r.x + (size_t)sj * r.dp;
-        const uint32_t ca = r.cnt[si], cb = r.cnt[sj];
-        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
-        for (int kk = lane; kk < d; kk += 64) {
-          const float v = consensus(xip[kk], fa, xj[kk], fb, fn);
-          sx[kk] = v;
-          xj[kk] = v;
-        }
-        __syncthreads();
-        if (lane == 0) {
-          float nn = 0.0f;
-          for (int kk = 0; kk < d; ++kk) nn = nn + sx[kk] * sx[kk];
-          r.nrm[sj] = nn;
-          link_members(r, si, sj);
-          mark_dirty(sj, w, ctr);
-          s[i] = s[size - 1];
-        }
-        __syncthreads();
-        --size;
-      } else {
+      if (found == 0xFFFFFFFFu) {
         ++i;
+        continue;
       }
+      // c[j] = SetConsensus(c[i], c[j]); c[i] = c[--size]  (cluster.cc:70-75)
+      const uint32_t sj = S[found];
+      const uint32_t ca = r.cnt[si], cb = r.cnt[sj];
+      const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+      float* xj = r.x + (size_t)sj * dp;
+      for (int k = (int)t; k < d; k += kHugeNT) {
+        const float v = consensus(xi[k], fa, xj[k], fb, fn);
+        xi[k] = v;  // the new row, for its norm
+        xj[k] = v;
+      }
+      __syncthreads();  // the new row is in memory and in LDS
+      if (t == 0) {
+        const float nn = dot_acc_mem(0.0f, xi, xi, d);  // distance.cc:33-34
+        r.nrm[sj] = nn;
+        if (in_lds) lq[found] = __builtin_sqrtf(nn);
+        link_members(r, si, sj);
+        mark_dirty(sj, w, ctr);
+        S[i] = S[size - 1];
+        if (in_lds) lq[i] = lq[size - 1];
+      }
+      __syncthreads();
+      --size;
     }
-    for (uint32_t t = size + lane; t < b; t += 64) s[t] = kInvalid;
+    if (in_lds)
+      for (uint32_t a = t; a < size; a += kHugeNT) slots[p + a] = ls[a];
+    for (uint32_t a = size + t; a < b; a += kHugeNT) slots[p + a] = kInvalid;
     __syncthreads();
   }
+}
+
+static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, const Rows& r,
+                        Counters* ctr, uint32_t n, hipStream_t s) {
+  const size_t lds = sizeof(uint32_t) * kHugeLdsRows * 2 + sizeof(float) * (size_t)r.dp;
+  static const bool lds_ok = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_huge),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
+  }();
+  (void)lds_ok;
+  const uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
+  k_merge_huge<<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
 }
 
 // ------------------------------------------------------------------ wide rows (any d) -----
@@ -1230,12 +1256,10 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
   const Fork f(w, s);
-  const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 1] + 1) + 1);
   // longest walks first on each stream
   launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(0));
   launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, f.lane(0));
-  k_merge_wave<D><<<g3, 64, sizeof(float) * r.dp, f.lane(0)>>>(w.huge, &ctr->n_huge, slots, dc, r,
-                                                               w, ctr);
+  launch_huge(w, slots, dc, r, ctr, n, f.lane(0));
   launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   k_merge_group<64, D><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
   k_merge_group<32, D><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
@@ -1268,11 +1292,9 @@ static void launch_groups_wide(const Rows& r, const uint32_t* seg, uint32_t hi, 
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
   const Fork f(w, s);
-  const uint32_t g3 = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 1] + 1) + 1);
   launch_big_wide<384, 256, 32>(w, 1, slots, dc, r, ctr, n, f.lane(0));
   launch_big_wide<896, 256, 16>(w, 2, slots, dc, r, ctr, n, f.lane(0));
-  k_merge_wave<0><<<g3, 64, sizeof(float) * r.dp, f.lane(0)>>>(w.huge, &ctr->n_huge, slots, dc, r,
-                                                               w, ctr);
+  launch_huge(w, slots, dc, r, ctr, n, f.lane(0));
   launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   k_merge_group_wide<64><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
   k_merge_group_wide<32><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
