@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "k-mers·iterations/sec (LSH+cluster loop), 10M k-mers × 64 samples"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_TFLOPS = 78.6  # packed f32 mul / add issue ceiling (see roofline["valu"])
 
 CONFIGS = {
     # name: (kmers, samples, iterations, min_similarity, description)
@@ -245,8 +246,13 @@ def main():
     avg_ms = agg["project_ms"] / max(1, launches)
     achieved = (proj_bytes / max(1, launches)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = pmc_traffic(args.config)
+    # the same launches against the packed-f32 VALU ceiling: one v_pk_mul + one v_pk_add per two
+    # row-hyperplane MACs (bit-exactness forbids fusing), 256 CU x 4 SIMD x 16 lanes x 2 x 2 flop
+    # x 2.4 GHz = 78.6 Tflop/s (half the FMA-counted 157.3 TF vector peak)
+    valu_flops = 2.0 * agg["sum_proj_bits"] * d / max(1, launches)
+    valu_achieved = valu_flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     roofline = {
-        "kernel": f"k_project<{d}>" if d in (8, 16, 32, 64) else "k_project_generic",
+        "kernel": f"k_project_pk<{d}>" if d in (8, 16, 32, 64) else "k_project_wide_pk",
         "bound": "hbm",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
@@ -257,6 +263,9 @@ def main():
         "bytes_per_launch": proj_bytes / max(1, launches),
         "avg_launch_ms": avg_ms,
         "launches_per_step": launches / args.steps,
+        "valu": {"achieved": round(valu_achieved, 2), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(valu_achieved / VALU_PEAK_TFLOPS, 4),
+                 "note": "separate f32 mul+add (no FMA: bit-exact with the reference), packed"},
     }
     cpu = None
     if world == 1:
