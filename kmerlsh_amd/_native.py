@@ -32,7 +32,7 @@ EXPORTED = (
     "klsh_load_counts", "klsh_snapshot", "klsh_restore", "klsh_cluster", "klsh_count",
     "klsh_result", "klsh_hash_keys", "klsh_pcluster", "klsh_hyperplanes", "klsh_fp_selftest",
     "klsh_synth_counts", "klsh_comm_unique_id", "klsh_comm_init", "klsh_comm_init_local",
-    "klsh_comm_info",
+    "klsh_comm_info", "klsh_set_option",
 )
 
 
@@ -108,6 +108,7 @@ def load_library() -> ctypes.CDLL:
         "klsh_comm_init_local": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
         "klsh_comm_info": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int),
                                           ctypes.POINTER(ctypes.c_int)]),
+        "klsh_set_option": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -217,6 +218,9 @@ class Engine:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         _check(self._lib.klsh_comm_init(self._ctx, rank, world, ctypes.cast(buf, ctypes.c_void_p)),
                "klsh_comm_init")
+
+    def set_option(self, name: str, value: int) -> None:
+        _check(self._lib.klsh_set_option(self._ctx, name.encode(), int(value)), "klsh_set_option")
 
     def comm_info(self) -> tuple[int, int]:
         r = ctypes.c_int(0)

@@ -153,6 +153,15 @@ struct klsh_ctx {
     return e && e[0] == '1';
   }();
 
+  // Sharded loop: below this many live rows the per-iteration exchanges cost more than they save
+  // (the late iterations are latency-bound on one GPU already), so every rank takes the whole
+  // canonical order and runs the remaining iterations on its replica — identically, with no
+  // communication.  klsh_set_option(ctx, "shard_min_rows", n); 0 = always sharded.
+  uint64_t shard_min_rows = [] {
+    const char* e = getenv("KLSH_SHARD_MIN_ROWS");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)(1u << 19);
+  }();
+
   int world() const { return comm ? comm->world : 1; }
   int rank() const { return comm ? comm->rank : 0; }
 
@@ -554,7 +563,8 @@ int klsh_restore(klsh_ctx* ctx) {
 // `out` (with ctx->mw.dlist set, the merge kernels also list the survivors they rewrote).
 // Ends with the counters on the host: total (survivors), n_over (oversize runs), n_delta.
 static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
-                      int bucket_thr, uint32_t* out, klsh_stats* st, bool timed) {
+                      int bucket_thr, uint32_t* out, klsh_stats* st, bool timed,
+                      bool sync = true) {
   hipStream_t s = ctx->stream;
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
   klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->mw, ctx->ctr, s);
@@ -563,6 +573,7 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
+  if (!sync) return 0;  // the caller fetches the counters with its own exchange
   if (int e = ctx->sync_counters()) return e;
   if (timed && st) {
     st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
@@ -642,268 +653,13 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
   return 0;
 }
 
-// ============================================================ sharded loop (DESIGN.md §7) ===
-// Every rank holds a replica of the rows; the canonical order of iteration t is the concatenation
-// over ranks of each rank's survivors ("mine").  Per iteration:
-//   project mine -> keys; bin histogram (top <= 12 key bits) -> allgather -> every rank derives
-//   the same bin -> rank ownership (contiguous key ranges balanced by rows) and send counts;
-//   stable partition of (key, slot) by owner -> all-to-all-v -> received pairs are in canonical
-//   order restricted to this rank's key range; stable radix sort by key = merge_hashtable's
-//   bucket order for those keys; greedy merge + compaction -> the new "mine"; the survivors a
-//   merge rewrote are broadcast (allgather-v of rows + metadata) so every replica stays identical.
-// Oversize buckets (nestedCluster) draw hyperplanes in ascending bucket order, i.e. rank order
-// then local order: a small allgather of (runs, hyperplanes) gives each rank its RNG offset.
-// Member links are written only by the rank that merged them; the end of the call combines them
-// with an element-wise min (an unwritten link is kNil = 0xFFFFFFFF) and gathers the global order.
-static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
-                           int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
-                           uint64_t* nt_trace, klsh_stats* st) {
-  klsh::Comm* cm = ctx->comm;
-  const int W = cm->world, g = cm->rank;
+// Iterations [it_begin, it_end) of the single-device loop over the whole canonical order
+// (cluster.cc:193-334).  `threshold` is advanced by sim_step per iteration.
+static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_begin, int it_end,
+                      int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
+                      uint64_t* nt_trace, klsh_stats* st) {
   hipStream_t s = ctx->stream;
-  if (int e = ctx->reserve_shard()) return e;
-  auto comm_fail = [&](const char* what) {
-    return fail(KLSH_E_HIP, std::string(what) + ": " + cm->err);
-  };
-  const double t_start = now_ms();
-  double t_comm = 0.0;
-  auto timed_comm = [&](auto fn) {
-    const double t0 = now_ms();
-    const int rc = fn();
-    t_comm += now_ms() - t0;
-    return rc;
-  };
-
-  const float max_similarity = 0.95f;  // cluster.cc:190-192 (all float)
-  const float sim_step = (max_similarity - min_similarity) / (float)iterations;
-  float threshold = max_similarity;
-
-  // my block of the global canonical order
-  uint64_t N = ctx->n_live;
-  uint32_t n_g = 0;
-  {
-    const uint64_t lo = N * (uint64_t)g / (uint64_t)W, hi = N * (uint64_t)(g + 1) / (uint64_t)W;
-    n_g = (uint32_t)(hi - lo);
-    if (n_g) KLSH_HIP(hipMemcpyAsync(ctx->alt, ctx->order + lo, 4ull * n_g, hipMemcpyDeviceToDevice, s));
-    std::swap(ctx->order, ctx->alt);
-  }
-  std::vector<uint32_t> n_all(W, 0);  // survivors per rank after the last exchange
-  for (int r = 0; r < W; ++r)
-    n_all[r] = (uint32_t)(N * (uint64_t)(r + 1) / W - N * (uint64_t)r / W);
-
-  ctx->w_count = 0;
-  if (N > 0 && iterations > 0) {
-    const uint64_t hmax = (uint64_t)floor_log2(N);
-    if (int e = ctx->ensure_hyperplanes(seed_base, *rng_counter, hmax * (uint64_t)iterations,
-                                        &st->host_ms))
-      return e;
-  }
-  const int R = klsh::delta_words(ctx->dp);
-  std::vector<size_t> scnt(W), soff(W), rcnt(W), roff(W), dcnt(W), doff(W);
-
-  for (int it = 0; it < iterations; ++it) {
-    if (nt_trace) nt_trace[it] = N;
-    st->iterations += 1;
-    if (N == 0) {
-      threshold -= sim_step;
-      continue;
-    }
-    const int h = floor_log2(N);
-    const uint64_t k = *rng_counter;
-    *rng_counter += (uint64_t)h;
-    st->hyperplanes += (uint64_t)h;
-    if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h, &st->host_ms)) return e;
-
-    // 1. keys of my rows, key-range ownership, send counts
-    KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
-    KLSH_HIP(hipEventRecord(ctx->ev[0], s));
-    klsh::launch_project(ctx->rows, ctx->order, ctx->keys, n_g, ctx->hyperplane_ptr(k), h, 0u, s);
-    KLSH_HIP(hipGetLastError());
-    KLSH_HIP(hipEventRecord(ctx->ev[1], s));
-    const int B = std::min(h, klsh::kMaxBinBits);
-    const int shift = h - B;
-    const uint32_t nbins = 1u << B;
-    klsh::launch_bin_hist(ctx->keys, n_g, shift, nbins, ctx->bins, s);
-    if (timed_comm([&] { return cm->allgather(ctx->bins, ctx->bins_all, 4ull * nbins, s); }))
-      return comm_fail("bin histogram allgather");
-    klsh::launch_bin_split(ctx->bins_all, W, nbins, N, ctx->owner, ctx->cntmat, s);
-    KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->cntmat, 4ull * W * W, hipMemcpyDeviceToHost, s));
-    KLSH_HIP(hipStreamSynchronize(s));
-    uint32_t m_g = 0;
-    for (int r = 0; r < W; ++r) {
-      scnt[r] = 8ull * ctx->h_small[g * W + r];
-      rcnt[r] = 8ull * ctx->h_small[r * W + g];
-      soff[r] = r ? soff[r - 1] + scnt[r - 1] : 0;
-      roff[r] = r ? roff[r - 1] + rcnt[r - 1] : 0;
-      m_g += ctx->h_small[r * W + g];
-    }
-
-    // 2. exchange (key, slot) pairs: stable partition by owner, all-to-all-v
-    uint32_t *dk = nullptr, *dv = nullptr;
-    klsh::launch_dest(ctx->keys, n_g, shift, ctx->owner, ctx->nk1, ctx->nk2, s);
-    klsh::radix_sort(ctx->nk1, ctx->nk2, ctx->nv2, ctx->keys2, n_g, 8, ctx->hist, ctx->tile_sums,
-                     ctx->ctr, &dk, &dv, s);
-    klsh::launch_pack_pairs(ctx->keys, ctx->order, dv, n_g, ctx->sbuf, s);
-    KLSH_HIP(hipGetLastError());
-    if (timed_comm([&] {
-          return cm->alltoallv(ctx->sbuf, scnt.data(), soff.data(), ctx->rbuf, rcnt.data(),
-                               roff.data(), s);
-        }))
-      return comm_fail("pair all-to-all");
-    klsh::launch_unpack_pairs(ctx->rbuf, m_g, ctx->keys, ctx->alt, s);
-    if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[6], s));
-
-    // 3. bucket order of my key range, merge, compaction, delta list
-    uint32_t *fk = nullptr, *fv = nullptr;
-    klsh::radix_sort(ctx->keys, ctx->alt, ctx->keys2, ctx->order, m_g, h, ctx->hist,
-                     ctx->tile_sums, ctx->ctr, &fk, &fv, s);
-    KLSH_HIP(hipGetLastError());
-    if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[5], s));
-    uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
-    ctx->mw.dlist = ctx->dslots;  // the merge kernels list the survivors they rewrite
-    ctx->mw.mark = ctx->mark;
-    ctx->mw.stamp = ++ctx->stamp;
-    const int rc_merge = merge_main(ctx, fk, fv, m_g, threshold, bucket_size_threshold, out, st,
-                                    ctx->phase_timing);
-    if (rc_merge) {
-      ctx->mw.dlist = nullptr;
-      return rc_merge;
-    }
-    std::vector<uint2> over;
-    uint64_t my_hyp = 0;
-    if (int e = oversize_runs(ctx, &over, &my_hyp)) return e;
-
-    // 4. counters of every rank: survivors, deltas, oversize runs and their hyperplanes
-    auto exchange_counters = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) -> int {
-      uint32_t* hs = ctx->h_small;
-      hs[0] = a; hs[1] = b; hs[2] = c; hs[3] = d;
-      KLSH_HIP(hipMemcpyAsync(ctx->small + 4 * W, hs, 16, hipMemcpyHostToDevice, s));
-      if (timed_comm([&] { return cm->allgather(ctx->small + 4 * W, ctx->small, 16, s); }))
-        return comm_fail("counter allgather");
-      KLSH_HIP(hipMemcpyAsync(hs, ctx->small, 16ull * W, hipMemcpyDeviceToHost, s));
-      KLSH_HIP(hipStreamSynchronize(s));
-      return 0;
-    };
-    if (int e = exchange_counters(ctx->h_ctr->total, ctx->h_ctr->n_delta, (uint32_t)over.size(),
-                                  (uint32_t)my_hyp))
-      return e;
-    std::vector<uint32_t> surv(W), ndel(W);
-    uint64_t any_over = 0, hyp_before = 0, hyp_all = 0;
-    for (int r = 0; r < W; ++r) {
-      surv[r] = ctx->h_small[4 * r];
-      ndel[r] = ctx->h_small[4 * r + 1];
-      any_over += ctx->h_small[4 * r + 2];
-      if (r < g) hyp_before += ctx->h_small[4 * r + 3];
-      hyp_all += ctx->h_small[4 * r + 3];
-    }
-    if (any_over) {
-      uint64_t rng = *rng_counter + hyp_before;
-      if (!over.empty()) {
-        const int rc_nested = merge_nested(ctx, fk, fv, m_g, threshold, over, seed_base, &rng, out, st);
-        if (rc_nested) {
-          ctx->mw.dlist = nullptr;
-          return rc_nested;
-        }
-      }
-      *rng_counter += hyp_all;
-      if (int e = exchange_counters(ctx->h_ctr->total, ctx->h_ctr->n_delta, 0, 0)) return e;
-      for (int r = 0; r < W; ++r) {
-        surv[r] = ctx->h_small[4 * r];
-        ndel[r] = ctx->h_small[4 * r + 1];
-      }
-    }
-
-    ctx->mw.dlist = nullptr;
-
-    // 5. merge deltas to every replica
-    uint64_t nd_all = 0;
-    for (int r = 0; r < W; ++r) {
-      dcnt[r] = 4ull * R * ndel[r];
-      doff[r] = 4ull * R * nd_all;
-      nd_all += ndel[r];
-    }
-    if (nd_all) {
-      if (int e = ctx->reserve_words(&ctx->drec, &ctx->drec_cap, (size_t)R * ndel[g] + 1)) return e;
-      if (int e = ctx->reserve_words(&ctx->drec_all, &ctx->drec_all_cap, (size_t)R * nd_all)) return e;
-      klsh::launch_delta_pack(ctx->rows, ctx->dslots, ndel[g], ctx->drec, s);
-      if (timed_comm([&] {
-            return cm->allgatherv(ctx->drec, ctx->drec_all, dcnt.data(), doff.data(), s);
-          }))
-        return comm_fail("delta allgather");
-      klsh::launch_delta_apply(ctx->rows, ctx->drec_all, (uint32_t)nd_all, s);
-      KLSH_HIP(hipGetLastError());
-    }
-
-    if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
-    const uint64_t N_next = std::accumulate(surv.begin(), surv.end(), (uint64_t)0);
-    st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
-    if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[6], ctx->ev[5]);
-    st->project_launches += 1;
-    st->sum_rows += N;
-    st->sum_proj_bits += N * (uint64_t)h;
-    st->sum_merges += N - N_next;
-    N = N_next;
-    n_g = surv[g];
-    n_all = surv;
-    threshold -= sim_step;
-  }
-
-  // global canonical order on every rank, combined member links
-  {
-    std::vector<size_t> cnt(W), off(W);
-    size_t acc = 0;
-    for (int r = 0; r < W; ++r) {
-      cnt[r] = 4ull * n_all[r];
-      off[r] = acc;
-      acc += cnt[r];
-    }
-    if (timed_comm([&] { return cm->allgatherv(ctx->order, ctx->alt, cnt.data(), off.data(), s); }))
-      return comm_fail("order allgather");
-    std::swap(ctx->order, ctx->alt);
-    if (timed_comm([&] { return cm->allreduce_min_u32(ctx->rows.nxt, ctx->members, s); }))
-      return comm_fail("member link allreduce");
-    KLSH_HIP(hipStreamSynchronize(s));
-  }
-  ctx->n_live = N;
-  st->n_final = N;
-  st->comm_ms = t_comm;
-  st->wall_ms = now_ms() - t_start;
-  return 0;
-}
-
-int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket_size_threshold,
-                 uint32_t seed_base, uint64_t* rng_counter, uint64_t* nt_trace, klsh_stats* stats) {
-  if (!ctx || !rng_counter) return fail(KLSH_E_ARG, "null argument");
-  if (!ctx->loaded) return fail(KLSH_E_STATE, "klsh_cluster before a load");
-  KLSH_HIP(hipSetDevice(ctx->device));
-  klsh_stats local{};
-  klsh_stats* st = stats ? stats : &local;
-  memset(st, 0, sizeof(*st));
-  st->world = (uint64_t)ctx->world();
-  if (ctx->comm)  // any bound group, world 1 included (measures the sharded machinery alone)
-    return cluster_sharded(ctx, min_similarity, iterations, bucket_size_threshold, seed_base,
-                           rng_counter, nt_trace, st);
-  const double t_start = now_ms();
-  hipStream_t s = ctx->stream;
-
-  // cluster.cc:190-192 (all float)
-  const float max_similarity = 0.95f;
-  const float sim_step = (max_similarity - min_similarity) / (float)iterations;
-  float threshold = max_similarity;
-
-  // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
-  // lshash.cc:36-42), so repeated timed calls never reuse a previous call's tables.
-  ctx->w_count = 0;
-  // Pre-draw the hyperplanes this call can need without nested buckets (h_t is non-increasing).
-  if (ctx->n_live > 0 && iterations > 0) {
-    const uint64_t hmax = (uint64_t)floor_log2(ctx->n_live);
-    if (int e = ctx->ensure_hyperplanes(seed_base, *rng_counter, hmax * (uint64_t)iterations,
-                                        &st->host_ms))
-      return e;
-  }
-
-  int it = 0;
-  for (; it < iterations; ++it) {
+  for (int it = it_begin; it < it_end; ++it) {
     const uint64_t n = ctx->n_live;
     if (nt_trace) nt_trace[it] = n;
     st->iterations += 1;
@@ -966,6 +722,301 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
     st->sum_merges += n - ctx->n_live;
     threshold -= sim_step;
   }
+  return 0;
+}
+
+// ============================================================ sharded loop (DESIGN.md §7) ===
+// Every rank holds a replica of the rows; the canonical order of iteration t is the concatenation
+// over ranks of each rank's survivors ("mine").  Per iteration:
+//   project mine -> keys; bin histogram (top <= 12 key bits) -> allgather -> every rank derives
+//   the same bin -> rank ownership (contiguous key ranges balanced by rows) and send counts;
+//   stable partition of (key, slot) by owner -> all-to-all-v -> received pairs are in canonical
+//   order restricted to this rank's key range; stable radix sort by key = merge_hashtable's
+//   bucket order for those keys; greedy merge + compaction -> the new "mine"; the survivors a
+//   merge rewrote are broadcast (allgather-v of rows + metadata) so every replica stays identical.
+// Oversize buckets (nestedCluster) draw hyperplanes in ascending bucket order, i.e. rank order
+// then local order: a small allgather of (runs, hyperplanes) gives each rank its RNG offset.
+// Member links are written only by the rank that merged them; the end of the call combines them
+// with an element-wise min (an unwritten link is kNil = 0xFFFFFFFF) and gathers the global order.
+static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
+                           int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
+                           uint64_t* nt_trace, klsh_stats* st) {
+  klsh::Comm* cm = ctx->comm;
+  const int W = cm->world, g = cm->rank;
+  hipStream_t s = ctx->stream;
+  if (int e = ctx->reserve_shard()) return e;
+  auto comm_fail = [&](const char* what) {
+    return fail(KLSH_E_HIP, std::string(what) + ": " + cm->err);
+  };
+  const double t_start = now_ms();
+  double t_comm = 0.0;
+  auto timed_comm = [&](auto fn) {
+    const double t0 = now_ms();
+    const int rc = fn();
+    t_comm += now_ms() - t0;
+    return rc;
+  };
+
+  const float max_similarity = 0.95f;  // cluster.cc:190-192 (all float)
+  const float sim_step = (max_similarity - min_similarity) / (float)iterations;
+  float threshold = max_similarity;
+
+  // my block of the global canonical order
+  uint64_t N = ctx->n_live;
+  uint32_t n_g = 0;
+  {
+    const uint64_t lo = N * (uint64_t)g / (uint64_t)W, hi = N * (uint64_t)(g + 1) / (uint64_t)W;
+    n_g = (uint32_t)(hi - lo);
+    if (n_g) KLSH_HIP(hipMemcpyAsync(ctx->alt, ctx->order + lo, 4ull * n_g, hipMemcpyDeviceToDevice, s));
+    std::swap(ctx->order, ctx->alt);
+  }
+  std::vector<uint32_t> n_all(W, 0);  // survivors per rank after the last exchange
+  for (int r = 0; r < W; ++r)
+    n_all[r] = (uint32_t)(N * (uint64_t)(r + 1) / W - N * (uint64_t)r / W);
+
+  ctx->w_count = 0;
+  if (N > 0 && iterations > 0) {
+    const uint64_t hmax = (uint64_t)floor_log2(N);
+    if (int e = ctx->ensure_hyperplanes(seed_base, *rng_counter, hmax * (uint64_t)iterations,
+                                        &st->host_ms))
+      return e;
+  }
+  const int R = klsh::delta_words(ctx->dp);
+  std::vector<size_t> scnt(W), soff(W), rcnt(W), roff(W), dcnt(W), doff(W);
+
+  bool replicated = false;
+  for (int it = 0; it < iterations; ++it) {
+    if (N < ctx->shard_min_rows) {  // the replicated tail: every rank runs the rest on its own
+      std::vector<size_t> cnt(W), off(W);
+      size_t acc = 0;
+      for (int r = 0; r < W; ++r) {
+        cnt[r] = 4ull * n_all[r];
+        off[r] = acc;
+        acc += cnt[r];
+      }
+      if (timed_comm([&] { return cm->allgatherv(ctx->order, ctx->alt, cnt.data(), off.data(), s); }))
+        return comm_fail("order allgather");
+      std::swap(ctx->order, ctx->alt);
+      ctx->n_live = N;
+      replicated = true;
+      if (int e = run_single(ctx, threshold, sim_step, it, iterations, bucket_size_threshold,
+                             seed_base, rng_counter, nt_trace, st))
+        return e;
+      N = ctx->n_live;
+      break;
+    }
+    if (nt_trace) nt_trace[it] = N;
+    st->iterations += 1;
+    if (N == 0) {
+      threshold -= sim_step;
+      continue;
+    }
+    const int h = floor_log2(N);
+    const uint64_t k = *rng_counter;
+    *rng_counter += (uint64_t)h;
+    st->hyperplanes += (uint64_t)h;
+    if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h, &st->host_ms)) return e;
+
+    // 1. keys of my rows, key-range ownership, send counts
+    KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    KLSH_HIP(hipEventRecord(ctx->ev[0], s));
+    klsh::launch_project(ctx->rows, ctx->order, ctx->keys, n_g, ctx->hyperplane_ptr(k), h, 0u, s);
+    KLSH_HIP(hipGetLastError());
+    KLSH_HIP(hipEventRecord(ctx->ev[1], s));
+    const int B = std::min(h, klsh::kMaxBinBits);
+    const int shift = h - B;
+    const uint32_t nbins = 1u << B;
+    klsh::launch_bin_hist(ctx->keys, n_g, shift, nbins, ctx->bins, s);
+    if (timed_comm([&] { return cm->allgather(ctx->bins, ctx->bins_all, 4ull * nbins, s); }))
+      return comm_fail("bin histogram allgather");
+    klsh::launch_bin_split(ctx->bins_all, W, nbins, N, ctx->owner, ctx->cntmat, s);
+    KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->cntmat, 4ull * W * W, hipMemcpyDeviceToHost, s));
+    KLSH_HIP(hipStreamSynchronize(s));
+    uint32_t m_g = 0;
+    for (int r = 0; r < W; ++r) {
+      scnt[r] = 8ull * ctx->h_small[g * W + r];
+      rcnt[r] = 8ull * ctx->h_small[r * W + g];
+      soff[r] = r ? soff[r - 1] + scnt[r - 1] : 0;
+      roff[r] = r ? roff[r - 1] + rcnt[r - 1] : 0;
+      m_g += ctx->h_small[r * W + g];
+    }
+
+    // 2. exchange (key, slot) pairs: stable partition by owner, all-to-all-v
+    uint32_t *dk = nullptr, *dv = nullptr;
+    klsh::launch_dest(ctx->keys, n_g, shift, ctx->owner, ctx->nk1, ctx->nk2, s);
+    klsh::radix_sort(ctx->nk1, ctx->nk2, ctx->nv2, ctx->keys2, n_g, 8, ctx->hist, ctx->tile_sums,
+                     ctx->ctr, &dk, &dv, s);
+    klsh::launch_pack_pairs(ctx->keys, ctx->order, dv, n_g, ctx->sbuf, s);
+    KLSH_HIP(hipGetLastError());
+    if (timed_comm([&] {
+          return cm->alltoallv(ctx->sbuf, scnt.data(), soff.data(), ctx->rbuf, rcnt.data(),
+                               roff.data(), s);
+        }))
+      return comm_fail("pair all-to-all");
+    klsh::launch_unpack_pairs(ctx->rbuf, m_g, ctx->keys, ctx->alt, s);
+    if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[6], s));
+
+    // 3. bucket order of my key range, merge, compaction, delta list
+    uint32_t *fk = nullptr, *fv = nullptr;
+    klsh::radix_sort(ctx->keys, ctx->alt, ctx->keys2, ctx->order, m_g, h, ctx->hist,
+                     ctx->tile_sums, ctx->ctr, &fk, &fv, s);
+    KLSH_HIP(hipGetLastError());
+    if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[5], s));
+    uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
+    ctx->mw.dlist = ctx->dslots;  // the merge kernels list the survivors they rewrite
+    ctx->mw.mark = ctx->mark;
+    ctx->mw.stamp = ++ctx->stamp;
+    const int rc_merge = merge_main(ctx, fk, fv, m_g, threshold, bucket_size_threshold, out, st,
+                                    ctx->phase_timing, /*sync=*/false);
+    if (rc_merge) {
+      ctx->mw.dlist = nullptr;
+      return rc_merge;
+    }
+    // 4. counters of every rank in one exchange and one host sync: oversize runs, survivors,
+    //    rewritten rows (n_over, total, n_delta are adjacent in Counters)
+    KLSH_HIP(hipMemcpyAsync(ctx->small + 4 * W, &ctx->ctr->n_over, 12, hipMemcpyDeviceToDevice, s));
+    if (timed_comm([&] { return cm->allgather(ctx->small + 4 * W, ctx->small, 16, s); }))
+      return comm_fail("counter allgather");
+    KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->small, 16ull * W, hipMemcpyDeviceToHost, s));
+    KLSH_HIP(hipMemcpyAsync(ctx->h_ctr, ctx->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    KLSH_HIP(hipStreamSynchronize(s));
+    if (ctx->phase_timing && st) {
+      st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
+      st->compact_ms += elapsed(ctx->ev[3], ctx->ev[4]);
+    }
+    std::vector<uint32_t> surv(W), ndel(W);
+    uint64_t any_over = 0;
+    for (int r = 0; r < W; ++r) {
+      any_over += ctx->h_small[4 * r];
+      surv[r] = ctx->h_small[4 * r + 1];
+      ndel[r] = ctx->h_small[4 * r + 2];
+    }
+    if (any_over) {  // nestedCluster somewhere: RNG offsets need every rank's hyperplane count
+      std::vector<uint2> over;
+      uint64_t my_hyp = 0;
+      if (int e = oversize_runs(ctx, &over, &my_hyp)) return e;
+      auto exchange_counters = [&](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) -> int {
+        uint32_t* hs = ctx->h_small;
+        hs[0] = a0; hs[1] = a1; hs[2] = a2; hs[3] = a3;
+        KLSH_HIP(hipMemcpyAsync(ctx->small + 4 * W, hs, 16, hipMemcpyHostToDevice, s));
+        if (timed_comm([&] { return cm->allgather(ctx->small + 4 * W, ctx->small, 16, s); }))
+          return comm_fail("counter allgather");
+        KLSH_HIP(hipMemcpyAsync(hs, ctx->small, 16ull * W, hipMemcpyDeviceToHost, s));
+        KLSH_HIP(hipStreamSynchronize(s));
+        return 0;
+      };
+      if (int e = exchange_counters((uint32_t)my_hyp, 0, 0, 0)) return e;
+      uint64_t hyp_before = 0, hyp_all = 0;
+      for (int r = 0; r < W; ++r) {
+        if (r < g) hyp_before += ctx->h_small[4 * r];
+        hyp_all += ctx->h_small[4 * r];
+      }
+      uint64_t rng = *rng_counter + hyp_before;
+      if (!over.empty()) {
+        const int rc_nested = merge_nested(ctx, fk, fv, m_g, threshold, over, seed_base, &rng, out, st);
+        if (rc_nested) {
+          ctx->mw.dlist = nullptr;
+          return rc_nested;
+        }
+      }
+      *rng_counter += hyp_all;
+      if (int e = exchange_counters(ctx->h_ctr->total, ctx->h_ctr->n_delta, 0, 0)) return e;
+      for (int r = 0; r < W; ++r) {
+        surv[r] = ctx->h_small[4 * r];
+        ndel[r] = ctx->h_small[4 * r + 1];
+      }
+    }
+    ctx->mw.dlist = nullptr;
+
+    // 5. merge deltas to every replica
+    uint64_t nd_all = 0;
+    for (int r = 0; r < W; ++r) {
+      dcnt[r] = 4ull * R * ndel[r];
+      doff[r] = 4ull * R * nd_all;
+      nd_all += ndel[r];
+    }
+    if (nd_all) {
+      if (int e = ctx->reserve_words(&ctx->drec, &ctx->drec_cap, (size_t)R * ndel[g] + 1)) return e;
+      if (int e = ctx->reserve_words(&ctx->drec_all, &ctx->drec_all_cap, (size_t)R * nd_all)) return e;
+      klsh::launch_delta_pack(ctx->rows, ctx->dslots, ndel[g], ctx->drec, s);
+      if (timed_comm([&] {
+            return cm->allgatherv(ctx->drec, ctx->drec_all, dcnt.data(), doff.data(), s);
+          }))
+        return comm_fail("delta allgather");
+      klsh::launch_delta_apply(ctx->rows, ctx->drec_all, (uint32_t)nd_all, s);
+      KLSH_HIP(hipGetLastError());
+    }
+
+    if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
+    const uint64_t N_next = std::accumulate(surv.begin(), surv.end(), (uint64_t)0);
+    st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
+    if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[6], ctx->ev[5]);
+    st->project_launches += 1;
+    st->sum_rows += N;
+    st->sum_proj_bits += N * (uint64_t)h;
+    st->sum_merges += N - N_next;
+    N = N_next;
+    n_g = surv[g];
+    n_all = surv;
+    threshold -= sim_step;
+  }
+
+  // global canonical order on every rank, combined member links
+  if (!replicated) {
+    std::vector<size_t> cnt(W), off(W);
+    size_t acc = 0;
+    for (int r = 0; r < W; ++r) {
+      cnt[r] = 4ull * n_all[r];
+      off[r] = acc;
+      acc += cnt[r];
+    }
+    if (timed_comm([&] { return cm->allgatherv(ctx->order, ctx->alt, cnt.data(), off.data(), s); }))
+      return comm_fail("order allgather");
+    std::swap(ctx->order, ctx->alt);
+  }
+  if (timed_comm([&] { return cm->allreduce_min_u32(ctx->rows.nxt, ctx->members, s); }))
+    return comm_fail("member link allreduce");
+  KLSH_HIP(hipStreamSynchronize(s));
+  ctx->n_live = N;
+  st->n_final = N;
+  st->comm_ms = t_comm;
+  st->wall_ms = now_ms() - t_start;
+  return 0;
+}
+
+int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket_size_threshold,
+                 uint32_t seed_base, uint64_t* rng_counter, uint64_t* nt_trace, klsh_stats* stats) {
+  if (!ctx || !rng_counter) return fail(KLSH_E_ARG, "null argument");
+  if (!ctx->loaded) return fail(KLSH_E_STATE, "klsh_cluster before a load");
+  KLSH_HIP(hipSetDevice(ctx->device));
+  klsh_stats local{};
+  klsh_stats* st = stats ? stats : &local;
+  memset(st, 0, sizeof(*st));
+  st->world = (uint64_t)ctx->world();
+  if (ctx->comm)  // any bound group, world 1 included (measures the sharded machinery alone)
+    return cluster_sharded(ctx, min_similarity, iterations, bucket_size_threshold, seed_base,
+                           rng_counter, nt_trace, st);
+  const double t_start = now_ms();
+
+  // cluster.cc:190-192 (all float)
+  const float max_similarity = 0.95f;
+  const float sim_step = (max_similarity - min_similarity) / (float)iterations;
+  float threshold = max_similarity;
+
+  // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
+  // lshash.cc:36-42), so repeated timed calls never reuse a previous call's tables.
+  ctx->w_count = 0;
+  // Pre-draw the hyperplanes this call can need without nested buckets (h_t is non-increasing).
+  if (ctx->n_live > 0 && iterations > 0) {
+    const uint64_t hmax = (uint64_t)floor_log2(ctx->n_live);
+    if (int e = ctx->ensure_hyperplanes(seed_base, *rng_counter, hmax * (uint64_t)iterations,
+                                        &st->host_ms))
+      return e;
+  }
+
+  if (int e = run_single(ctx, threshold, sim_step, 0, iterations, bucket_size_threshold, seed_base,
+                         rng_counter, nt_trace, st))
+    return e;
   st->n_final = ctx->n_live;
   st->wall_ms = now_ms() - t_start;
   return 0;
@@ -1003,6 +1054,21 @@ int klsh_comm_init_local(klsh_ctx** ctxs, int world) {
     ctxs[r]->comm = cs[r];
   }
   return 0;
+}
+
+int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx || !name) return fail(KLSH_E_ARG, "null argument");
+  const std::string n(name);
+  if (n == "shard_min_rows") {
+    if (value < 0) return fail(KLSH_E_ARG, "shard_min_rows must be >= 0");
+    ctx->shard_min_rows = (uint64_t)value;
+    return 0;
+  }
+  if (n == "phase_timing") {
+    ctx->phase_timing = value != 0;
+    return 0;
+  }
+  return fail(KLSH_E_ARG, "unknown option " + n);
 }
 
 int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world) {

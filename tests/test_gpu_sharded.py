@@ -21,16 +21,18 @@ def same_bits(a, b):
                           np.ascontiguousarray(b, np.float32).view(np.uint32))
 
 
-def run_group(world, load, calls):
+def run_group(world, load, calls, shard_min_rows=0):
     """Create `world` engines on device 0, load each with load(eng), bind them into one group,
     run the klsh_cluster calls (list of argument tuples) on every rank concurrently.  Returns
-    per-rank lists of (trace, counter, stats) and the per-rank results."""
+    per-rank lists of (trace, counter, stats) and the per-rank results.  shard_min_rows = 0
+    keeps every iteration sharded; larger values switch to the replicated tail below it."""
     from kmerlsh_amd import _native
 
     engines = [_native.Engine(0) for _ in range(world)]
     try:
         for e in engines:
             load(e)
+            e.set_option("shard_min_rows", shard_min_rows)
         _native.comm_init_local(engines)
         for r, e in enumerate(engines):
             assert e.comm_info() == (r, world)
@@ -132,6 +134,19 @@ def test_sharded_random_vs_single(engine, world, n, d, groups, iters, bthr):
     calls = [(0.8, iters, bthr, 777, 3)]
     ref = single(engine, lambda e: e.load_rows(rows), calls)
     outs, results = run_group(world, lambda e: e.load_rows(rows), calls)
+    for r in range(world):
+        assert_same(outs[r], results[r], *ref)
+
+
+@pytest.mark.parametrize("world,switch", [(2, 150000), (3, 120000), (4, 1 << 19)])
+def test_sharded_then_replicated_tail_vs_single(engine, world, switch):
+    """The crossover: sharded while N_t >= switch, then every rank runs the rest on its replica."""
+    rng = np.random.default_rng(world * 7 + 1)
+    rows = clustered(rng, 200000, 64, 30000, 0.05)
+    calls = [(0.8, 15, 1000000, 777, 3)]
+    ref = single(engine, lambda e: e.load_rows(rows), calls)
+    assert ref[0][0][0][0] >= switch or switch > 200000  # the run starts sharded unless above n
+    outs, results = run_group(world, lambda e: e.load_rows(rows), calls, shard_min_rows=switch)
     for r in range(world):
         assert_same(outs[r], results[r], *ref)
 
