@@ -172,3 +172,24 @@ def test_sharded_empty_and_single_row():
     outs, res = run_group(3, lambda e: e.load_rows(np.ones((1, 8), np.float32)), calls)
     assert [list(o[0][0]) for o in outs] == [[1, 1, 1]] * 3
     assert all(r[0].shape == (1, 8) for r in res)
+
+
+def test_rccl_single_rank_group_vs_single(engine):
+    """The RCCL backend itself (a one-rank communicator: its allgather, broadcast-based
+    allgather-v, all-to-all self copy and min all-reduce) driving the sharded loop."""
+    from kmerlsh_amd import _native
+
+    rng = np.random.default_rng(11)
+    rows = clustered(rng, 100000, 64, 2000, 0.05)
+    calls = [(0.8, 10, 1000000, 5, 0)]
+    ref = single(engine, lambda e: e.load_rows(rows), calls)
+    eng = _native.Engine(0)
+    try:
+        eng.load_rows(rows)
+        eng.comm_init(0, 1, _native.comm_unique_id())
+        eng.set_option("shard_min_rows", 0)
+        trace, counter, st = eng.cluster(*calls[0])
+        assert st["world"] == 1 and st["comm_ms"] > 0.0
+        assert_same([(trace, counter, st)], eng.result(), *ref)
+    finally:
+        eng.close()
