@@ -439,15 +439,92 @@ __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restric
   }
 }
 
+// The same stable scatter, staged: the tile is first ordered by digit in LDS (positions from the
+// tile's own digit counts, ranks as in k_radix_scatter), then written out by consecutive lanes —
+// each digit's keys of the tile land in one contiguous run of the output instead of 2048
+// scattered 4-byte writes.
+__global__ __launch_bounds__(256) void k_radix_scatter_lds(const uint32_t* __restrict__ kin,
+                                                           const uint32_t* __restrict__ vin,
+                                                           uint32_t* __restrict__ kout,
+                                                           uint32_t* __restrict__ vout, uint32_t n,
+                                                           int shift, uint32_t ntiles,
+                                                           const uint32_t* __restrict__ hist) {
+  __shared__ uint32_t lk[kRadixTile], lv[kRadixTile];
+  __shared__ uint32_t gbase[256];   // global offset of the tile's first key of each digit
+  __shared__ uint32_t lstart[256];  // tile-local offset of each digit
+  __shared__ uint32_t run[256];     // keys of each digit placed so far
+  __shared__ uint32_t wcnt[4][256];
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint32_t tile0 = blockIdx.x * (uint32_t)kRadixTile;
+  const uint32_t m = min((uint32_t)kRadixTile, n - tile0);
+  // global offsets of the tile's digits (the scanned [digit][tile] histogram)
+  gbase[t] = hist[t * ntiles + blockIdx.x];
+  run[t] = 0;
+  wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+  __syncthreads();
+  // local digit counts: atomics in LDS
+  for (uint32_t i = t; i < m; i += 256) atomicAdd(&wcnt[0][(kin[tile0 + i] >> shift) & 255u], 1u);
+  __syncthreads();
+  {
+    uint32_t total;
+    lstart[t] = block_excl_scan_256(wcnt[0][t], &total);
+  }
+  wcnt[0][t] = 0;
+  __syncthreads();
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int r = 0; r < kRadixTile / 256; ++r) {
+    const uint32_t i = r * 256u + t;
+    const bool valid = i < m;
+    const uint32_t k = valid ? kin[tile0 + i] : 0u;
+    const uint32_t v = valid ? vin[tile0 + i] : 0u;
+    const uint32_t dig = (k >> shift) & 255u;
+    uint64_t match = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (dig >> b) & 1u;
+      const uint64_t mb = __ballot(bit);
+      match &= bit ? mb : ~mb;
+    }
+    const uint32_t rank = __popcll(match & lt_mask);
+    if (valid && rank == 0) wcnt[w][dig] = __popcll(match);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = lstart[dig] + run[dig] + rank;
+      for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dig];
+      lk[pos] = k;
+      lv[pos] = v;
+    }
+    __syncthreads();
+    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+    __syncthreads();
+  }
+  // write out in LDS order: entry e of digit d goes to gbase[d] + (e - lstart[d])
+  for (uint32_t e = t; e < m; e += 256) {
+    const uint32_t k = lk[e];
+    const uint32_t d = (k >> shift) & 255u;
+    const uint32_t pos = gbase[d] + (e - lstart[d]);
+    kout[pos] = k;
+    vout[pos] = lv[e];
+  }
+}
+
 void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
                 uint32_t* hist, uint32_t* tile_sums, Counters* ctr, uint32_t** out_k,
                 uint32_t** out_v, hipStream_t s) {
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
   const uint32_t ntiles = (n + kRadixTile - 1) / kRadixTile;
+  static const bool scatter_lds = [] {  // KLSH_SCATTER=direct: the unstaged scatter
+    const char* e = getenv("KLSH_SCATTER");
+    return !(e && std::string(e) == "direct");
+  }();
   for (int shift = 0; shift < bits && n > 1; shift += 8) {
     k_radix_hist<<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, hist);
     device_scan(SrcArray{hist}, DstExclusive{hist}, 256u * ntiles, tile_sums, &ctr->total, s);
-    k_radix_scatter<<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, hist);
+    if (scatter_lds)
+      k_radix_scatter_lds<<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, hist);
+    else
+      k_radix_scatter<<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, hist);
     uint32_t* t;
     t = ki; ki = ko; ko = t;
     t = vi; vi = vo; vo = t;
