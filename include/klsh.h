@@ -123,6 +123,12 @@ int klsh_result(klsh_ctx* ctx, float* rows, uint64_t* member_offsets, uint64_t* 
  * GPU: keys[i] = MSB-first sign bits of the h hyperplanes (table: h x d, row-major). */
 int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const float* table, int h,
                    uint32_t* keys);
+/* merge_hashtable (reference function/cluster.cc:15-30) on the GPU: the stable bucket order of n
+ * keys by their low `bits` bits (keys must be < 2^bits for a pure bucket order; higher bits are
+ * carried along unsorted).  sorted_keys[i] = keys[perm[i]]; perm lists original positions, equal
+ * keys in their original order. */
+int klsh_bucket_sort(klsh_ctx* ctx, const uint32_t* keys, uint64_t n, int bits,
+                     uint32_t* sorted_keys, uint32_t* perm);
 /* p_cluster (reference function/cluster.cc:56-87) over the loaded rows taken as ONE bucket in
  * load order, at threshold thr.  Afterwards klsh_count/klsh_result give the survivors. */
 int klsh_pcluster(klsh_ctx* ctx, float thr);

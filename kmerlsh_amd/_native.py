@@ -30,7 +30,7 @@ ERRORS = {
 EXPORTED = (
     "klsh_create", "klsh_destroy", "klsh_last_error", "klsh_version", "klsh_load_rows",
     "klsh_load_counts", "klsh_snapshot", "klsh_restore", "klsh_cluster", "klsh_count",
-    "klsh_result", "klsh_hash_keys", "klsh_pcluster", "klsh_hyperplanes", "klsh_fp_selftest",
+    "klsh_result", "klsh_hash_keys", "klsh_bucket_sort", "klsh_pcluster", "klsh_hyperplanes", "klsh_fp_selftest",
     "klsh_synth_counts", "klsh_comm_unique_id", "klsh_comm_init", "klsh_comm_init_local",
     "klsh_comm_info", "klsh_set_option",
 )
@@ -97,6 +97,7 @@ def load_library() -> ctypes.CDLL:
         "klsh_result": (ctypes.c_int, [_P, _P, _P, _P]),
         "klsh_hash_keys": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, _P,
                                           ctypes.c_int, _P]),
+        "klsh_bucket_sort": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, _P, _P]),
         "klsh_pcluster": (ctypes.c_int, [_P, ctypes.c_float]),
         "klsh_hyperplanes": (ctypes.c_int, [ctypes.c_uint32, _u64p, ctypes.c_int,
                                             ctypes.c_int, _P]),
@@ -259,6 +260,15 @@ class Engine:
         _check(self._lib.klsh_hash_keys(self._ctx, _ptr(rows), n, d, _ptr(table), h,
                                         _ptr(keys)), "klsh_hash_keys")
         return keys
+
+    def bucket_sort(self, keys: np.ndarray, bits: int):
+        """merge_hashtable's stable bucket order on the GPU: (sorted keys, permutation)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        out = np.zeros_like(keys)
+        perm = np.zeros_like(keys)
+        _check(self._lib.klsh_bucket_sort(self._ctx, _ptr(keys), keys.size, bits, _ptr(out),
+                                          _ptr(perm)), "klsh_bucket_sort")
+        return out, perm
 
     def fp_selftest(self, a: np.ndarray, b: np.ndarray):
         a = np.ascontiguousarray(a, np.float32)

@@ -255,17 +255,201 @@ __global__ __launch_bounds__(256) void k_scan_apply(Src src, Dst dst, uint32_t n
   }
 }
 
+// ------------------------------------------------------------ single-pass scan (look-back) ----
+// Tiles are taken in ticket order (atomic counter), so a tile only ever waits on tiles that are
+// already running.  Each tile publishes its aggregate at once, then its inclusive prefix once the
+// look-back (one wave, 64 predecessors per step) has found one.  Status words carry an epoch
+// (one per scan launch, kept on the device), so stale words of earlier scans read as "not yet" and
+// the status array never needs clearing; the last workgroup to finish resets the ticket and
+// advances the epoch.  A wait that exceeds kSpinLimit polls (a broken invariant, never expected)
+// sets *err and gives up instead of hanging the GPU.
+constexpr uint32_t kStatusAgg = 1u, kStatusPrefix = 2u;
+constexpr uint32_t kEpochMask = 0x3FFFFFFFu;
+constexpr uint32_t kSpinLimit = 1u << 22;
+// Scan workspace (the engine's tile_sums buffer): words [0] ticket, [1] done, [2] epoch, then the
+// 64-bit tile status array from word kScanStatusWord.
+constexpr uint32_t kScanStatusWord = 64;
+
+__device__ __forceinline__ uint64_t status_pack(uint32_t epoch, uint32_t flag, uint32_t value) {
+  return ((uint64_t)((epoch << 2) | flag) << 32) | value;
+}
+__device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t status_load(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// flag of a status word if it belongs to `epoch`, else 0 (not published yet)
+__device__ __forceinline__ uint32_t status_flag(uint64_t v, uint32_t epoch) {
+  const uint32_t hi = (uint32_t)(v >> 32);
+  return (hi >> 2) == epoch ? (hi & 3u) : 0u;
+}
+
+// Exclusive prefix of tile `tile` (> 0) from the status words of tiles [0, tile): called by all
+// 64 lanes of one wave; every lane returns the same value.
+__device__ __forceinline__ uint32_t lookback_wave(const uint64_t* status, uint32_t tile,
+                                                  uint32_t epoch, uint32_t* err) {
+  const uint32_t lane = __lane_id();
+  uint32_t excl = 0;
+  int64_t j = (int64_t)tile - 1;  // lane l looks at tile j - l
+  uint32_t spins = 0;
+  while (true) {
+    const int64_t idx = j - (int64_t)lane;
+    uint64_t v = 0;
+    uint32_t f = kStatusPrefix;  // before tile 0: an empty prefix
+    if (idx >= 0) {
+      v = status_load(status + idx);
+      f = status_flag(v, epoch);
+    }
+    while (__ballot(f == 0u)) {  // some predecessor has published nothing yet
+      if (++spins > kSpinLimit) {
+        if (lane == 0) atomicOr(err, 1u);
+        return excl;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (f == 0u) {
+        v = status_load(status + idx);
+        f = status_flag(v, epoch);
+      }
+    }
+    const uint64_t pm = __ballot(f == kStatusPrefix);
+    const uint32_t stop = pm ? (uint32_t)__builtin_ctzll(pm) : 63u;  // nearest prefix (or all 64)
+    uint32_t c = (lane <= stop && idx >= 0) ? (uint32_t)v : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    excl += c;
+    if (pm) return excl;
+    j -= 64;
+  }
+}
+
 template <class Src, class Dst>
-inline void device_scan(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, uint32_t* total,
-                        hipStream_t s) {
+__global__ __launch_bounds__(256) void k_scan_lb(Src src, Dst dst, uint32_t n, uint32_t* ws,
+                                                 uint32_t* total, uint32_t* err) {
+  __shared__ uint32_t s_tile, s_epoch, s_excl;
+  const uint32_t t = threadIdx.x;
+  uint64_t* status = reinterpret_cast<uint64_t*>(ws + kScanStatusWord);
+  if (t == 0) {
+    s_tile = atomicAdd(&ws[0], 1u);
+    s_epoch = (ws[2] + 1u) & kEpochMask;
+  }
+  __syncthreads();
+  const uint32_t tile = s_tile, epoch = s_epoch;
+  const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
+  if (tile < ntiles) {
+    const uint32_t base = tile * (uint32_t)kScanTile + t * 16u;
+    uint32_t v[16];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      v[k] = (base + k < n) ? src(base + k) : 0u;
+      acc += v[k];
+    }
+    uint32_t tsum;
+    const uint32_t in_tile = block_excl_scan_256(acc, &tsum);
+    if (t == 0) status_store(status + tile, status_pack(epoch, tile == 0 ? kStatusPrefix : kStatusAgg, tsum));
+    if (t < 64) {
+      const uint32_t excl = tile == 0 ? 0u : lookback_wave(status, tile, epoch, err);
+      if (t == 0) {
+        if (tile > 0) status_store(status + tile, status_pack(epoch, kStatusPrefix, excl + tsum));
+        s_excl = excl;
+        if (tile == ntiles - 1) *total = excl + tsum;
+      }
+    }
+    __syncthreads();
+    uint32_t run = s_excl + in_tile;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (base + k < n) dst(base + k, run, v[k]);
+      run += v[k];
+    }
+  } else if (tile == 0) {  // n == 0
+    if (t == 0) *total = 0;
+  }
+  // the last workgroup out resets the ticket and moves the epoch on
+  if (t == 0) {
+    if (atomicAdd(&ws[1], 1u) == gridDim.x - 1) {
+      atomicExch(&ws[0], 0u);
+      atomicExch(&ws[1], 0u);
+      atomicExch(&ws[2], epoch);
+    }
+  }
+}
+
+// Three-kernel variant (tile sums, one-workgroup scan of them, apply); KLSH_SCAN=3k selects it.
+template <class Src, class Dst>
+inline void device_scan_3k(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, uint32_t* total,
+                           hipStream_t s) {
   const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
   if (ntiles == 0) {
     (void)hipMemsetAsync(total, 0, sizeof(uint32_t), s);
     return;
   }
-  k_scan_tile_sum<Src><<<ntiles, 256, 0, s>>>(src, n, tile_sums);
-  k_scan_tiles<0><<<1, 1024, 0, s>>>(tile_sums, ntiles, total);
-  k_scan_apply<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, tile_sums);
+  uint32_t* ts = tile_sums + kScanStatusWord;  // keep the look-back words intact
+  k_scan_tile_sum<Src><<<ntiles, 256, 0, s>>>(src, n, ts);
+  k_scan_tiles<0><<<1, 1024, 0, s>>>(ts, ntiles, total);
+  k_scan_apply<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, ts);
+}
+
+// Two-kernel variant: tile sums, then every tile sums the tile sums before it itself (ntiles^2/2
+// L2-resident reads in all: no single-workgroup scan, no waiting between workgroups).
+template <class Src, class Dst>
+__global__ __launch_bounds__(256) void k_scan_apply_redundant(Src src, Dst dst, uint32_t n,
+                                                              const uint32_t* __restrict__ tile_sums,
+                                                              uint32_t* total) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t t = threadIdx.x, tile = blockIdx.x;
+  uint32_t before = 0;
+  for (uint32_t i = t; i < tile; i += 256) before += tile_sums[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+  if ((t & 63u) == 0) wsum[t >> 6] = before;
+  __syncthreads();
+  before = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  const uint32_t base = tile * (uint32_t)kScanTile + t * 16u;
+  uint32_t v[16];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = (base + k < n) ? src(base + k) : 0u;
+    acc += v[k];
+  }
+  uint32_t tsum;
+  uint32_t run = block_excl_scan_256(acc, &tsum) + before;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (base + k < n) dst(base + k, run, v[k]);
+    run += v[k];
+  }
+  if (tile == gridDim.x - 1 && t == 0) *total = before + tsum;
+}
+
+template <class Src, class Dst>
+inline void device_scan_2k(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, uint32_t* total,
+                           hipStream_t s) {
+  const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
+  if (ntiles == 0) {
+    (void)hipMemsetAsync(total, 0, sizeof(uint32_t), s);
+    return;
+  }
+  uint32_t* ts = tile_sums + kScanStatusWord;
+  k_scan_tile_sum<Src><<<ntiles, 256, 0, s>>>(src, n, ts);
+  k_scan_apply_redundant<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, ts, total);
+}
+
+int scan_variant();  // KLSH_SCAN: 0 look-back (default), 1 two-kernel, 2 three-kernel
+
+
+// Exclusive scan of src over [0, n) feeding dst(i, prefix, value); *total = sum.  `ws` is the
+// scan workspace (zeroed once at allocation, kScanStatusWord + 2 * ceil(n / kScanTile) words).
+template <class Src, class Dst>
+inline void device_scan(Src src, Dst dst, uint32_t n, uint32_t* ws, uint32_t* total,
+                        uint32_t* err, hipStream_t s) {
+  const int var = scan_variant();
+  if (var == 1) return device_scan_2k(src, dst, n, ws, total, s);
+  if (var == 2) return device_scan_3k(src, dst, n, ws, total, s);
+  const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
+  k_scan_lb<Src, Dst><<<ntiles ? ntiles : 1u, 256, 0, s>>>(src, dst, n, ws, total, err);
 }
 
 }  // namespace klsh

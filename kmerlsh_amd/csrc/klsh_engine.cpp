@@ -142,6 +142,7 @@ struct klsh_ctx {
   uint32_t* drec_all = nullptr;
   size_t drec_cap = 0, drec_all_cap = 0;  // words
   uint64_t shard_cap = 0;
+  double t_enqueued = 0.0;  // diagnostics (KLSH_ITER_LOG): host time when an iteration was queued
 
   ~klsh_ctx() { release(); }
 
@@ -270,7 +271,7 @@ struct klsh_ctx {
         (e = dalloc(&order, s)) || (e = dalloc(&alt, s)) || (e = dalloc(&keys, s)) ||
         (e = dalloc(&keys2, s)) || (e = dalloc(&nk1, s)) || (e = dalloc(&nk2, s)) ||
         (e = dalloc(&nv2, s)) ||
-        (e = dalloc(&hist, 256 * ((s + klsh::kRadixTile - 1) / klsh::kRadixTile) + 256)) ||
+        (e = dalloc(&hist, klsh::sort_ws_words(s))) ||
         (e = dalloc(&tile_sums, (256 * s) / klsh::kScanTile + 1024)) ||
         (e = dalloc(&mw.seg, s + 64)) || (e = dalloc(&mw.over, s + 64)) ||
         (e = dalloc(&mw.big[0], s / 65 + 64)) || (e = dalloc(&mw.big[1], s / 129 + 64)) ||
@@ -283,6 +284,13 @@ struct klsh_ctx {
         release_state();
         return e;
       }
+    }
+    // the look-back workspaces start zeroed (tickets, done counters, epochs, histograms) and the
+    // kernels return them to zero; they are never cleared again
+    if (hipMemset(hist, 0, sizeof(uint32_t) * klsh::sort_ws_words(s)) != hipSuccess ||
+        hipMemset(tile_sums, 0, sizeof(uint32_t) * ((256 * s) / klsh::kScanTile + 1024)) != hipSuccess) {
+      release_state();
+      return fail(KLSH_E_HIP, "workspace init");
     }
     mw.tile_sums = tile_sums;
     cap_slots = s;
@@ -331,6 +339,12 @@ struct klsh_ctx {
   int sync_counters() {
     KLSH_HIP(hipMemcpyAsync(h_ctr, ctr, sizeof(Counters), hipMemcpyDeviceToHost, stream));
     KLSH_HIP(hipStreamSynchronize(stream));
+    return check_device_err();
+  }
+  int check_device_err() const {
+    if (h_ctr->err)
+      return fail(KLSH_E_HIP, "device protocol failure (look-back wait limit), code " +
+                                  std::to_string(h_ctr->err));
     return 0;
   }
 };
@@ -389,6 +403,7 @@ klsh_ctx* klsh_create(int device, int* err) {
   ok = ok && hipEventCreateWithFlags(&c->mw.fork, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->ctr, sizeof(Counters)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) == hipSuccess;
+  ok = ok && hipMemset(c->ctr, 0, sizeof(Counters)) == hipSuccess;  // err starts clear
   if (!ok) {
     delete c;
     fail(KLSH_E_HIP, "stream/event/counter allocation failed");
@@ -490,6 +505,10 @@ int klsh_load_counts(klsh_ctx* ctx, const uint16_t* counts, uint64_t n_total,
       rc = fail(KLSH_E_HIP, "lut upload");
       break;
     }
+    if (hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s) != hipSuccess) {
+      rc = fail(KLSH_E_HIP, "counter reset");
+      break;
+    }
     klsh::launch_convert(ctx->rows, dcounts, (uint32_t)bs, dlut, dv, ctx->keys, ctx->order,
                          ctx->tile_sums, ctx->ctr, s);
     if (hipGetLastError() != hipSuccess) {
@@ -574,6 +593,7 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
   if (!sync) return 0;  // the caller fetches the counters with its own exchange
+  ctx->t_enqueued = now_ms();
   if (int e = ctx->sync_counters()) return e;
   if (timed && st) {
     st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
@@ -659,8 +679,13 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
                       int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
                       uint64_t* nt_trace, klsh_stats* st) {
   hipStream_t s = ctx->stream;
+  static FILE* iter_log = [] {  // diagnostics: per-iteration wall time (it, n, h, ms)
+    const char* e = getenv("KLSH_ITER_LOG");
+    return e ? fopen(e, "a") : nullptr;
+  }();
   for (int it = it_begin; it < it_end; ++it) {
     const uint64_t n = ctx->n_live;
+    const double t_it = iter_log ? now_ms() : 0.0;
     if (nt_trace) nt_trace[it] = n;
     st->iterations += 1;
     if (n == 0) {  // the reference aborts here (cluster.cc:194 on an empty vector); no-op
@@ -721,7 +746,11 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     st->sum_proj_bits += n * (uint64_t)h;
     st->sum_merges += n - ctx->n_live;
     threshold -= sim_step;
+    if (iter_log)
+      fprintf(iter_log, "%d %llu %d %.4f %.4f\n", it, (unsigned long long)n, h, now_ms() - t_it,
+              ctx->t_enqueued - t_it);
   }
+  if (iter_log) fflush(iter_log);
   return 0;
 }
 
@@ -880,6 +909,7 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
     KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->small, 16ull * W, hipMemcpyDeviceToHost, s));
     KLSH_HIP(hipMemcpyAsync(ctx->h_ctr, ctx->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
     KLSH_HIP(hipStreamSynchronize(s));
+    if (int e = ctx->check_device_err()) return e;
     if (ctx->phase_timing && st) {
       st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
       st->compact_ms += elapsed(ctx->ev[3], ctx->ev[4]);
@@ -1171,6 +1201,54 @@ int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const fl
   }
   (void)hipStreamSynchronize(s);
   dfree(r.x); dfree(slots); dfree(dkeys); dfree(W);
+  return rc;
+}
+
+int klsh_bucket_sort(klsh_ctx* ctx, const uint32_t* keys, uint64_t n, int bits,
+                     uint32_t* sorted_keys, uint32_t* perm) {
+  if (!ctx || (n && (!keys || !sorted_keys || !perm))) return fail(KLSH_E_ARG, "null argument");
+  if (bits < 0 || bits > 32) return fail(KLSH_E_RANGE, "bits out of range");
+  if (n >= 0xFFFFFFF0ull) return fail(KLSH_E_RANGE, "keys >= 2^32");
+  if (n == 0) return 0;
+  KLSH_HIP(hipSetDevice(ctx->device));
+  uint32_t *k0 = nullptr, *v0 = nullptr, *k1 = nullptr, *v1 = nullptr, *ws = nullptr, *ts = nullptr;
+  Counters* ctr = nullptr;
+  const uint64_t ts_words = (256 * n) / klsh::kScanTile + 1024;
+  int e = 0;
+  auto release = [&] {
+    dfree(k0); dfree(v0); dfree(k1); dfree(v1); dfree(ws); dfree(ts); dfree(ctr);
+  };
+  if ((e = dalloc(&k0, n)) || (e = dalloc(&v0, n)) || (e = dalloc(&k1, n)) || (e = dalloc(&v1, n)) ||
+      (e = dalloc(&ws, klsh::sort_ws_words(n))) || (e = dalloc(&ts, ts_words)) ||
+      (e = dalloc(&ctr, 1))) {
+    release();
+    return e;
+  }
+  hipStream_t s = ctx->stream;
+  std::vector<uint32_t> iota(n);
+  for (uint64_t i = 0; i < n; ++i) iota[i] = (uint32_t)i;
+  Counters hc{};
+  int rc = 0;
+  uint32_t *ok = nullptr, *ov = nullptr;
+  if (hipMemsetAsync(ws, 0, sizeof(uint32_t) * klsh::sort_ws_words(n), s) != hipSuccess ||
+      hipMemsetAsync(ts, 0, sizeof(uint32_t) * ts_words, s) != hipSuccess ||
+      hipMemsetAsync(ctr, 0, sizeof(Counters), s) != hipSuccess ||
+      hipMemcpyAsync(k0, keys, 4 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(v0, iota.data(), 4 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+    rc = fail(KLSH_E_HIP, "upload");
+  } else {
+    klsh::radix_sort(k0, v0, k1, v1, (uint32_t)n, bits, ws, ts, ctr, &ok, &ov, s);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(sorted_keys, ok, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(perm, ov, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&hc, ctr, sizeof(Counters), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = fail(KLSH_E_HIP, "sort");
+    else if (hc.err)
+      rc = fail(KLSH_E_HIP, "device protocol failure in the sort");
+  }
+  (void)hipStreamSynchronize(s);
+  release();
   return rc;
 }
 

@@ -12,6 +12,13 @@ constexpr uint32_t kNil = 0xFFFFFFFFu;      // end of a member list
 constexpr int kMaxHyperplanes = 32;         // keys are uint32 (h = floor(log2 N) <= 31)
 constexpr int kRadixTile = 2048;            // keys per radix-sort workgroup (256 lanes x 8 rounds)
 constexpr int kScanTile = 4096;             // items per scan workgroup (256 lanes x 16)
+constexpr uint32_t kSortStatusWord = 2048;  // sort workspace: small words, then tile status
+// Sort workspace words for `slots` keys (onesweep: 256 u64 status words per tile) and scan
+// workspace words (64 small words + one u64 status word per scan tile; at least what the
+// three-kernel scan variant needs).  Both are zeroed once at allocation.
+inline uint64_t sort_ws_words(uint64_t slots) {
+  return kSortStatusWord + 512ull * ((slots + kRadixTile - 1) / kRadixTile) + 256;
+}
 
 // Bucket runs of 65..896 rows are merged by one workgroup with the run's decision matrix in LDS
 // (k_merge_big; three size classes, rows in LDS up to 384); longer runs by one wave from memory
@@ -33,7 +40,8 @@ struct Counters {
   uint32_t n_over;                 // runs longer than bucket_size_threshold (nestedCluster)
   uint32_t total;                  // result of the last scan/compaction (live rows)
   uint32_t n_delta;                // sharded loop: survivors rewritten by a merge this iteration
-  uint32_t pad[2];
+  uint32_t err;                    // a device-side protocol failure (look-back wait limit); 0 = ok
+  uint32_t pad;
 };
 
 // Merge workspace (device), sized for `cap` positions.

@@ -1309,7 +1309,7 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   if (hi <= lo) return;
   const uint32_t n = hi - lo;
   const Decider dc = make_decider(thr);
-  device_scan(SrcHead{key, lo}, DstSegStart{w.seg, lo}, n, w.tile_sums, &ctr->n_seg, s);
+  device_scan(SrcHead{key, lo}, DstSegStart{w.seg, lo}, n, w.tile_sums, &ctr->n_seg, &ctr->err, s);
   switch (r.d) {
     case 8: launch_groups<8>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
     case 16: launch_groups<16>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;

@@ -54,6 +54,33 @@ def test_hash_keys_match_reference(engine, name):
     assert np.array_equal(engine.hash_keys(z["rows"], w), z["keys"])
 
 
+@pytest.mark.parametrize("n,bits,spread", [
+    (1, 8, 1), (2, 1, 2), (2047, 8, 300), (2048, 13, 1 << 13), (2049, 16, 5),
+    (100_000, 17, 1 << 17), (300_000, 23, 1000), (1_000_003, 22, 1 << 22), (5_000_000, 23, 1 << 23),
+    (200_000, 31, 1 << 31), (70_000, 0, 1),
+])
+def test_bucket_sort_is_stable_counting_sort(engine, n, bits, spread):
+    """merge_hashtable (cluster.cc:15-30) scatters rows into lsh_table[key] in row order: the
+    stable bucket order, i.e. numpy's stable argsort of the keys (single-pass look-back sort)."""
+    rng = np.random.default_rng(n + bits)
+    keys = rng.integers(0, spread, n, dtype=np.uint64).astype(np.uint32)
+    if bits < 32:
+        keys &= np.uint32((1 << bits) - 1) if bits else np.uint32(0)
+    got_k, got_p = engine.bucket_sort(keys, bits)
+    want = np.argsort(keys, kind="stable")
+    assert np.array_equal(got_p, want.astype(np.uint32))
+    assert np.array_equal(got_k, keys[want])
+
+
+def test_bucket_sort_repeated_calls(engine):
+    """several sorts of different sizes in a row on one context"""
+    rng = np.random.default_rng(5)
+    for n in (300_000, 4_096, 1, 2_500_000, 65_537):
+        keys = rng.integers(0, 1 << 20, n, dtype=np.uint32)
+        k, p = engine.bucket_sort(keys, 20)
+        assert np.array_equal(p, np.argsort(keys, kind="stable").astype(np.uint32))
+
+
 def test_hash_keys_random_vs_oracle(engine, oracle):
     from kmerlsh_amd import _native
 
