@@ -437,7 +437,7 @@ inline void device_scan_2k(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, ui
   k_scan_apply_redundant<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, ts, total);
 }
 
-int scan_variant();  // KLSH_SCAN: 0 look-back (default), 1 two-kernel, 2 three-kernel
+int scan_variant();  // KLSH_SCAN: 0 auto (default), 1 "2k", 2 "3k", 3 "lb" (look-back at any size)
 
 
 // Exclusive scan of src over [0, n) feeding dst(i, prefix, value); *total = sum.  `ws` is the
@@ -445,7 +445,11 @@ int scan_variant();  // KLSH_SCAN: 0 look-back (default), 1 two-kernel, 2 three-
 template <class Src, class Dst>
 inline void device_scan(Src src, Dst dst, uint32_t n, uint32_t* ws, uint32_t* total,
                         uint32_t* err, hipStream_t s) {
-  const int var = scan_variant();
+  // auto: the look-back kernel below 2^20 items (one launch; as fast as the others there), the
+  // two-kernel scan above (tools/ubench_sort on MI355X: 18.5 vs 15.9 us at 1M, 201 vs 87 us at
+  // 9.47M — look-back chains across ~2000 co-resident tiles)
+  int var = scan_variant();
+  if (var == 0 && n >= (1u << 20)) var = 1;
   if (var == 1) return device_scan_2k(src, dst, n, ws, total, s);
   if (var == 2) return device_scan_3k(src, dst, n, ws, total, s);
   const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;

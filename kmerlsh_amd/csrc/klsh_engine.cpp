@@ -1049,6 +1049,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
     return e;
   st->n_final = ctx->n_live;
   st->wall_ms = now_ms() - t_start;
+  if (getenv("KLSH_MERGE_PROF")) klsh::merge_prof_dump(stderr);
   return 0;
 }
 

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
+#include <stdio.h>
 
 namespace klsh {
 
@@ -87,10 +88,17 @@ struct Rows {
 // Fast path (`fast` != 0, s_star a positive normal float): q = dot * rcp(den) is within 2 ulp of
 // dot / den, so q >= s_hi (s_star + 8 ulp) or q <= s_lo (s_star - 8 ulp) settles the test and only
 // quotients within a few ulp of s_star take the correctly rounded division.
+// Pre-screen (`fast` only): a Gram value G from the bf16x3 MFMA tiles (kGramMargin below) settles
+// the test when G / den >= g_hi or <= g_lo; pairs in between take the exact sequential dot.
 struct Decider {
   float s_star, s_lo, s_hi;
   uint32_t fast;
+  float g_lo, g_hi;
 };
+// |G - dot| <= 6.3e-5 * |a| |b| for the bf16x3 Gram value (hi/lo split, 3 MFMAs, f32
+// accumulation of 3d terms, d <= 64) against the reference's sequential f32 dot; the margin adds
+// headroom for den's rounding and the approximate quotient.
+constexpr float kGramMargin = 1.5e-4f;
 Decider make_decider(float thr);
 
 // ---- launch wrappers (all asynchronous on `s`) ------------------------------------------------
@@ -157,6 +165,9 @@ __host__ __device__ inline int delta_words(int dp) { return 5 + dp; }
 void launch_delta_pack(const Rows& r, const uint32_t* delta_slots, uint32_t n, uint32_t* rec,
                        hipStream_t s);
 void launch_delta_apply(const Rows& r, const uint32_t* rec, uint32_t n, hipStream_t s);
+// Merge profile of the diagnostics build (-DKLSH_MERGE_PROF): print and clear.
+void merge_prof_dump(FILE* f);
+
 // a[i] = min(a[i], b[i])
 void launch_min_u32(uint32_t* a, const uint32_t* b, size_t n, hipStream_t s);
 

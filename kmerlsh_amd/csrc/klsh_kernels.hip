@@ -684,7 +684,7 @@ int scan_variant() {
     const char* e = getenv("KLSH_SCAN");
     if (!e) return 0;
     const std::string x(e);
-    return x == "2k" ? 1 : x == "3k" ? 2 : 0;
+    return x == "2k" ? 1 : x == "3k" ? 2 : x == "lb" ? 3 : 0;
   }();
   return v;
 }

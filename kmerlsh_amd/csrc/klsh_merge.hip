@@ -42,6 +42,25 @@ __device__ __forceinline__ void wave_lds_fence() {
   // from moving LDS accesses across this point (no wait for outstanding global stores)
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
+// KLSH_GRAM_TILES=0 at build time keeps the exact all-pairs VALU tiles everywhere (A/B).
+#ifndef KLSH_GRAM_TILES
+#define KLSH_GRAM_TILES 1
+#endif
+constexpr bool kGramTiles = KLSH_GRAM_TILES != 0;
+
+// Merge profiling (diagnostics build only: -DKLSH_MERGE_PROF, make prof): per size class, the
+// runs, rows, merges and wall-clock ticks (100 MHz) of each phase, summed over the call.
+#ifdef KLSH_MERGE_PROF
+__device__ unsigned long long g_mprof[8][8];
+#define MPROF_T() wall_clock64()
+#define MPROF_ADD(c, k, v) atomicAdd(&g_mprof[c][k], (unsigned long long)(v))
+#define MPROF_MAX(c, k, v) atomicMax(&g_mprof[c][k], (unsigned long long)(v))
+#else
+#define MPROF_T() 0ull
+#define MPROF_ADD(c, k, v) (void)0
+#define MPROF_MAX(c, k, v) (void)0
+#endif
+
 __device__ __forceinline__ void lds_barrier() {
   // workgroup barrier for LDS data only: this wave's LDS stores have landed (lgkmcnt(0)), then
   // s_barrier — without the vmcnt(0) wait of __syncthreads for outstanding global stores
@@ -455,6 +474,146 @@ __global__ __launch_bounds__(256) void k_merge_pair(const uint2* __restrict__ li
 // 64-row column block at a time for the decision phase).  The matrix is kept in POSITION space:
 // P[y] bit q = decide(row y, row at position q), so the walk's "first j < i" is a
 // find-first-set over W words, and positions that find nothing are skipped in bulk.
+// ---------------------------------------------------------------- MFMA pre-screen -----
+// The all-pairs decisions of a run are a Gram matrix X X^T (b x b x d).  The matrix cores compute
+// it with a bf16x3 split (x = hi + lo, hi = bf16(x), lo = bf16(x - hi); G = hi.hi + hi.lo + lo.hi
+// accumulated in f32), within kGramMargin * |a||b| of the reference's sequential f32 dot — so
+// G / den settles every pair whose quotient is not within the margin of s*; the few that are
+// take the exact sequential dot (the reference's order), so every decision is still bit-exact.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void split8(const float* p, bool ok, bf16x8& hi, bf16x8& lo) {
+  float x[8];
+  if (ok) {
+    const float4 u = *reinterpret_cast<const float4*>(p);
+    const float4 v = *reinterpret_cast<const float4*>(p + 4);
+    x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w;
+    x[4] = v.x; x[5] = v.y; x[6] = v.z; x[7] = v.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = 0.0f;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)x[j];
+    hi[j] = h;
+    lo[j] = (__bf16)(x[j] - (float)h);  // x - hi is exact in f32
+  }
+}
+
+// Pre-screen of one pair from its Gram value: 1 = merge, 0 = no merge, 2 = too close to call
+// (or den outside the fast range): the exact sequential dot decides.
+__device__ __forceinline__ uint32_t prescreen(const Decider& dc, float g, float den) {
+  if (den >= 0x1p-60f && den <= 0x1p60f) {
+    const float q = g * __builtin_amdgcn_rcpf(den);
+    if (q >= dc.g_hi) return 1u;
+    if (q <= dc.g_lo) return 0u;
+  }
+  return 2u;
+}
+
+// One wave: the decisions of rows [R*64, R*64+64) against rows [C*64, C*64+64) (C <= R; pairs
+// c < a only), ORed into the position-space matrix P (W words per row, both P[a] bit c and
+// P[c] bit a).  rowA(a) / rowB(c) give the rows (LDS or memory); D = d, a multiple of 16.
+template <int D, class RowA, class RowB>
+__device__ __forceinline__ void gram_tile(uint32_t R, uint32_t C, uint32_t b, RowA rowA, RowB rowB,
+                                          const float* sq, const Decider& dc, uint64_t* P, int W) {
+  const uint32_t lane = __lane_id(), r = lane & 31u, h = lane >> 5;
+  const uint32_t a0 = R * 64u, c0 = C * 64u;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.0f;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const uint32_t a = a0 + m * 32u + r, c = c0 + m * 32u + r;
+      split8(a < b ? rowA(a) + 16 * s + 8 * h : nullptr, a < b, ah[m], al[m]);
+      split8(c < b ? rowB(c) + 16 * s + 8 * h : nullptr, c < b, bh[m], bl[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[m], bh[n], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[m], bl[n], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[m], bh[n], acc[m][n], 0, 0, 0);
+      }
+  }
+  // decisions: acc[m][n][i] is G[a][c] with a = a0 + 32m + (i&3) + 8(i>>2) + 4h, c = c0 + 32n + r;
+  // bit e = 32m + 16n + i of hitm / ambm
+  uint64_t hitm = 0ull, ambm = 0ull;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t a = a0 + 32u * m + (i & 3) + 8u * (i >> 2) + 4u * h;
+        const uint32_t c = c0 + 32u * n + r;
+        if (a < b && c < a) {
+          const uint32_t v = prescreen(dc, acc[m][n][i], sq[a] * sq[c]);
+          const int e = 32 * m + 16 * n + i;
+          hitm |= (uint64_t)(v & 1u) << e;
+          ambm |= (uint64_t)(v >> 1) << e;
+        }
+      }
+  while (ambm) {  // rare: the exact sequential dot (the reference's order) decides
+    const int e = __builtin_ctzll(ambm);
+    ambm &= ambm - 1ull;
+    const int m = e >> 5, n = (e >> 4) & 1, i = e & 15;
+    const uint32_t a = a0 + 32u * m + (i & 3) + 8u * (i >> 2) + 4u * h;
+    const uint32_t c = c0 + 32u * n + r;
+    const float* pa = rowA(a);
+    const float* pc = rowB(c);
+    float sdot = 0.0f;
+    for (int k = 0; k < D; k += 4) {
+      const float4 u = *reinterpret_cast<const float4*>(pa + k);
+      const float4 v = *reinterpret_cast<const float4*>(pc + k);
+      sdot = sdot + u.x * v.x;
+      sdot = sdot + u.y * v.y;
+      sdot = sdot + u.z * v.z;
+      sdot = sdot + u.w * v.w;
+    }
+    if (decide(dc, sdot, sq[a] * sq[c])) hitm |= 1ull << e;
+  }
+  uint64_t tmask[2] = {0ull, 0ull};  // column c0+32n+r: bits over the 64 rows of block R
+  uint64_t own = 0ull;                // lane L ends up with the word of row a0 + L
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t ar = 32u * m + (i & 3) + 8u * (i >> 2) + 4u * h;  // row within the block
+      uint64_t bal[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const bool hit = (hitm >> (32 * m + 16 * n + i)) & 1ull;
+        tmask[n] |= (hit ? 1ull : 0ull) << ar;
+        bal[n] = __ballot(hit);
+      }
+      // rows r0 (lanes with h = 0) and r0 + 4 (h = 1): their 64-bit words over the block's columns
+      const uint32_t r0 = 32u * m + (i & 3) + 8u * (i >> 2);
+      const uint64_t w0 = (bal[0] & 0xFFFFFFFFull) | (bal[1] << 32);
+      const uint64_t w1 = (bal[0] >> 32) | (bal[1] & 0xFFFFFFFF00000000ull);
+      if (lane == r0) own = w0;
+      if (lane == r0 + 4u) own = w1;
+    }
+  }
+  if (own && a0 + lane < b) atomicOr((unsigned long long*)&P[(a0 + lane) * W + C], (unsigned long long)own);
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const uint64_t full = tmask[n] | shfl64(tmask[n], lane ^ 32u);
+    const uint32_t c = c0 + 32u * n + r;
+    if (h == 0 && full && c < b) atomicOr((unsigned long long*)&P[c * W + R], (unsigned long long)full);
+  }
+}
+
 // s + sequential sum of a[e] * b[e], e < n, a and b in memory (16-B aligned rows)
 __device__ __forceinline__ float dot_acc_mem(float s, const float* a, const float* b, int n) {
   int k = 0;
@@ -657,6 +816,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
     const uint2 e = list[li];
     const uint32_t p = e.x, b = e.y;
     const uint32_t nblk = (b + 63) / 64;
+    [[maybe_unused]] const uint64_t pt0 = MPROF_T();
     for (uint32_t a = t; a < b; a += NT) {
       const uint32_t s = slots[p + a];
       slot[a] = s;
@@ -709,13 +869,32 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
       }
       if (a < b && own) atomicOr((unsigned long long*)&P[a * W + C], (unsigned long long)own);
     };
+    const bool gram = kGramTiles && D % 16 == 0 && dc.fast;  // uniform
     if constexpr (ROWS_LDS) {
       const uint32_t ntiles = nblk * (nblk + 1) / 2;
       for (uint32_t ti = wv; ti < ntiles; ti += NW) {
         uint32_t R = 0;
         while ((R + 1) * (R + 2) / 2 <= ti) ++R;
         const uint32_t C = ti - R * (R + 1) / 2;
+        if constexpr (D % 16 == 0) {
+          if (gram) {
+            auto rl = [&](uint32_t a) -> const float* { return rows + a * ST; };
+            gram_tile<D>(R, C, b, rl, rl, sq, dc, P, W);
+            continue;
+          }
+        }
         tile(R, C, rows + C * 64u * ST);
+      }
+    } else if (gram) {
+      if constexpr (D % 16 == 0) {
+        auto rm = [&](uint32_t a) -> const float* { return r.x + (size_t)slot[a] * r.dp; };
+        const uint32_t ntiles = nblk * (nblk + 1) / 2;
+        for (uint32_t ti = wv; ti < ntiles; ti += NW) {
+          uint32_t R = 0;
+          while ((R + 1) * (R + 2) / 2 <= ti) ++R;
+          const uint32_t C = ti - R * (R + 1) / 2;
+          gram_tile<D>(R, C, b, rm, rm, sq, dc, P, W);
+        }
       }
     } else {
       for (uint32_t C = 0; C < nblk; ++C) {
@@ -731,10 +910,24 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
       }
     }
     __syncthreads();
-
+    [[maybe_unused]] const uint64_t pt1 = MPROF_T();
     big_walk<RB, NT, ROWS_LDS>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq,
                                ROWS_LDS ? rows : nullptr, ST, rows, wbuf, r, dc, slots, dlist, ctr);
     __syncthreads();
+#ifdef KLSH_MERGE_PROF
+    if (t == 0) {
+      const uint64_t pt2 = MPROF_T();
+      uint32_t live = 0;
+      for (uint32_t q = 0; q < b; ++q) live += slots[p + q] != kInvalid ? 1u : 0u;
+      MPROF_ADD(cls, 0, 1);
+      MPROF_ADD(cls, 1, b);
+      MPROF_ADD(cls, 2, b - live);
+      MPROF_ADD(cls, 3, pt1 - pt0);
+      MPROF_ADD(cls, 4, pt2 - pt1);
+      MPROF_MAX(cls, 5, pt2 - pt0);
+      MPROF_MAX(cls, 6, b);
+    }
+#endif
   }
 }
 
@@ -764,6 +957,7 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
     const uint2 e = list[li];
     const uint32_t p = e.x, b = e.y;
     const bool in_lds = b <= kHugeLdsRows;
+    [[maybe_unused]] const uint64_t pt0 = MPROF_T();
     uint32_t* S = in_lds ? ls : slots + p;
     if (in_lds)
       for (uint32_t a = t; a < b; a += kHugeNT) {
@@ -834,6 +1028,14 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
       for (uint32_t a = t; a < size; a += kHugeNT) slots[p + a] = ls[a];
     for (uint32_t a = size + t; a < b; a += kHugeNT) slots[p + a] = kInvalid;
     __syncthreads();
+    if (t == 0) {
+      MPROF_ADD(3, 0, 1);
+      MPROF_ADD(3, 1, b);
+      MPROF_ADD(3, 2, b - size);
+      MPROF_ADD(3, 4, MPROF_T() - pt0);
+      MPROF_MAX(3, 5, MPROF_T() - pt0);
+      MPROF_MAX(3, 6, b);
+    }
   }
 }
 
@@ -1083,6 +1285,7 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__
     const uint2 e = list[li];
     const uint32_t p = e.x, b = e.y;
     const uint32_t nblk = (b + 63) / 64;
+    [[maybe_unused]] const uint64_t pt0 = MPROF_T();
     for (uint32_t a = t; a < b; a += NT) {
       const uint32_t s = slots[p + a];
       slot[a] = s;
@@ -1183,7 +1386,7 @@ static float from_ordered(uint32_t o) {
 }
 
 Decider make_decider(float thr) {
-  Decider dc{std::numeric_limits<float>::quiet_NaN(), 0.0f, 0.0f, 0u};
+  Decider dc{std::numeric_limits<float>::quiet_NaN(), 0.0f, 0.0f, 0u, 0.0f, 0.0f};
   uint32_t lo = ordered(-std::numeric_limits<float>::infinity());
   uint32_t hi = ordered(std::numeric_limits<float>::infinity());
   if (!(sim_roundtrip(from_ordered(hi)) >= thr)) return dc;  // nothing passes (thr NaN)
@@ -1197,6 +1400,8 @@ Decider make_decider(float thr) {
     dc.s_lo = from_ordered(hi - 8);
     dc.s_hi = from_ordered(hi + 8);
     dc.fast = 1u;
+    dc.g_lo = dc.s_star - kGramMargin;
+    dc.g_hi = dc.s_star + kGramMargin;
   }
   return dc;
 }
@@ -1317,6 +1522,26 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
     case 64: launch_groups<64>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
     default: launch_groups_wide(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s);
   }
+}
+
+
+// Prints and clears the merge profile (diagnostics build only; a no-op otherwise).
+void merge_prof_dump(FILE* f) {
+#ifdef KLSH_MERGE_PROF
+  unsigned long long h[8][8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mprof), sizeof(h)) != hipSuccess) return;
+  const char* names[4] = {"big128", "big384", "big896", "huge"};
+  for (int c = 0; c < 4; ++c)
+    if (h[c][0])
+      fprintf(f, "[mprof] %-7s runs %8llu rows %10llu merges %9llu  load+tiles %9.3f ms  walk %9.3f ms"
+                 "  (per run %7.2f + %7.2f us)  max run %8.2f us  max b %llu\n",
+              names[c], h[c][0], h[c][1], h[c][2], h[c][3] * 1e-5, h[c][4] * 1e-5,
+              h[c][3] * 1e-2 / h[c][0], h[c][4] * 1e-2 / h[c][0], h[c][5] * 1e-2, h[c][6]);
+  unsigned long long z[8][8] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mprof), z, sizeof(z));
+#else
+  (void)f;
+#endif
 }
 
 }  // namespace klsh
