@@ -267,8 +267,7 @@ constexpr uint32_t kStatusAgg = 1u, kStatusPrefix = 2u;
 constexpr uint32_t kEpochMask = 0x3FFFFFFFu;
 constexpr uint32_t kSpinLimit = 1u << 22;
 // Scan workspace (the engine's tile_sums buffer): words [0] ticket, [1] done, [2] epoch, then the
-// 64-bit tile status array from word kScanStatusWord.
-constexpr uint32_t kScanStatusWord = 64;
+// 64-bit tile status array from word kScanStatusWord (klsh_internal.h: scan_ws_words).
 
 __device__ __forceinline__ uint64_t status_pack(uint32_t epoch, uint32_t flag, uint32_t value) {
   return ((uint64_t)((epoch << 2) | flag) << 32) | value;
@@ -385,7 +384,7 @@ inline void device_scan_3k(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, ui
     (void)hipMemsetAsync(total, 0, sizeof(uint32_t), s);
     return;
   }
-  uint32_t* ts = tile_sums + kScanStatusWord;  // keep the look-back words intact
+  uint32_t* ts = tile_sums + kScanSumsWord;  // apart from the look-back words
   k_scan_tile_sum<Src><<<ntiles, 256, 0, s>>>(src, n, ts);
   k_scan_tiles<0><<<1, 1024, 0, s>>>(ts, ntiles, total);
   k_scan_apply<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, ts);
@@ -432,7 +431,7 @@ inline void device_scan_2k(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, ui
     (void)hipMemsetAsync(total, 0, sizeof(uint32_t), s);
     return;
   }
-  uint32_t* ts = tile_sums + kScanStatusWord;
+  uint32_t* ts = tile_sums + kScanSumsWord;
   k_scan_tile_sum<Src><<<ntiles, 256, 0, s>>>(src, n, ts);
   k_scan_apply_redundant<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, ts, total);
 }
@@ -441,7 +440,7 @@ int scan_variant();  // KLSH_SCAN: 0 auto (default), 1 "2k", 2 "3k", 3 "lb" (loo
 
 
 // Exclusive scan of src over [0, n) feeding dst(i, prefix, value); *total = sum.  `ws` is the
-// scan workspace (zeroed once at allocation, kScanStatusWord + 2 * ceil(n / kScanTile) words).
+// scan workspace (zeroed once at allocation, scan_ws_words(n) words).
 template <class Src, class Dst>
 inline void device_scan(Src src, Dst dst, uint32_t n, uint32_t* ws, uint32_t* total,
                         uint32_t* err, hipStream_t s) {

@@ -272,7 +272,7 @@ struct klsh_ctx {
         (e = dalloc(&keys2, s)) || (e = dalloc(&nk1, s)) || (e = dalloc(&nk2, s)) ||
         (e = dalloc(&nv2, s)) ||
         (e = dalloc(&hist, klsh::sort_ws_words(s))) ||
-        (e = dalloc(&tile_sums, (256 * s) / klsh::kScanTile + 1024)) ||
+        (e = dalloc(&tile_sums, klsh::scan_ws_words(s))) ||
         (e = dalloc(&mw.seg, s + 64)) || (e = dalloc(&mw.over, s + 64)) ||
         (e = dalloc(&mw.big[0], s / 65 + 64)) || (e = dalloc(&mw.big[1], s / 129 + 64)) ||
         (e = dalloc(&mw.big[2], s / 385 + 64)) || (e = dalloc(&mw.huge, s / 897 + 64))) {
@@ -288,7 +288,7 @@ struct klsh_ctx {
     // the look-back workspaces start zeroed (tickets, done counters, epochs, histograms) and the
     // kernels return them to zero; they are never cleared again
     if (hipMemset(hist, 0, sizeof(uint32_t) * klsh::sort_ws_words(s)) != hipSuccess ||
-        hipMemset(tile_sums, 0, sizeof(uint32_t) * ((256 * s) / klsh::kScanTile + 1024)) != hipSuccess) {
+        hipMemset(tile_sums, 0, sizeof(uint32_t) * klsh::scan_ws_words(s)) != hipSuccess) {
       release_state();
       return fail(KLSH_E_HIP, "workspace init");
     }
@@ -396,8 +396,15 @@ klsh_ctx* klsh_create(int device, int* err) {
   c->device = device;
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
   for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  // the big-run merge stream gets the highest priority: its workgroups need a whole CU's LDS and
+  // would otherwise wait behind the small-run waves (KLSH_BIG_PRIORITY=0: all equal)
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  const char* bp = getenv("KLSH_BIG_PRIORITY");
+  const bool big_prio = !(bp && bp[0] == '0');
   for (int i = 0; i < klsh::kMergeStreams; ++i) {
-    ok = ok && hipStreamCreateWithFlags(&c->mw.aux[i], hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipStreamCreateWithPriority(&c->mw.aux[i], hipStreamNonBlocking,
+                                           (i == 0 && big_prio) ? prio_hi : prio_lo) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&c->mw.join[i], hipEventDisableTiming) == hipSuccess;
   }
   ok = ok && hipEventCreateWithFlags(&c->mw.fork, hipEventDisableTiming) == hipSuccess;
@@ -1153,7 +1160,11 @@ int klsh_result(klsh_ctx* ctx, float* rows, uint64_t* member_offsets, uint64_t* 
     uint64_t m = 0;
     for (uint64_t i = 0; i < n; ++i) {
       if (member_offsets) member_offsets[i] = m;
+      if (ord[i] >= ctx->slots) return fail(KLSH_E_STATE, "corrupt live order");
       for (uint32_t node = head[ord[i]]; node != klsh::kNil; node = nxt[node]) {
+        // every member belongs to exactly one live row: a longer walk is a broken list
+        if (node >= ctx->members || m >= ctx->members)
+          return fail(KLSH_E_STATE, "corrupt member list");
         if (member_ids) member_ids[m] = ctx->ids[node];
         ++m;
       }
@@ -1214,7 +1225,7 @@ int klsh_bucket_sort(klsh_ctx* ctx, const uint32_t* keys, uint64_t n, int bits,
   KLSH_HIP(hipSetDevice(ctx->device));
   uint32_t *k0 = nullptr, *v0 = nullptr, *k1 = nullptr, *v1 = nullptr, *ws = nullptr, *ts = nullptr;
   Counters* ctr = nullptr;
-  const uint64_t ts_words = (256 * n) / klsh::kScanTile + 1024;
+  const uint64_t ts_words = klsh::scan_ws_words(n);
   int e = 0;
   auto release = [&] {
     dfree(k0); dfree(v0); dfree(k1); dfree(v1); dfree(ws); dfree(ts); dfree(ctr);

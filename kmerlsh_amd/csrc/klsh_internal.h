@@ -20,6 +20,14 @@ constexpr uint32_t kSortStatusWord = 2048;  // sort workspace: small words, then
 inline uint64_t sort_ws_words(uint64_t slots) {
   return kSortStatusWord + 512ull * ((slots + kRadixTile - 1) / kRadixTile) + 256;
 }
+// Scan workspace (u32 words): [0, 64) ticket / done / epoch of the look-back scan, then its 64-bit
+// tile status words (room for 2^32 items), then the tile sums of the multi-kernel scans and of
+// the compaction — apart, so a tile sum can never pass for a look-back status word.
+constexpr uint32_t kScanStatusWord = 64;
+constexpr uint64_t kScanSumsWord = kScanStatusWord + 2ull * (1ull << 20);
+inline uint64_t scan_ws_words(uint64_t slots) {
+  return kScanSumsWord + (256 * slots) / kScanTile + 1024;
+}
 
 // Bucket runs of 65..896 rows are merged by one workgroup with the run's decision matrix in LDS
 // (k_merge_big; three size classes, rows in LDS up to 384); longer runs by one wave from memory

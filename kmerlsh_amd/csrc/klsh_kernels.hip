@@ -370,9 +370,79 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
   }
 }
 
+// Stable compaction of the live slots (merge_abundance's concatenation, cluster.cc:39-45) in two
+// coalesced passes: per-tile live counts (wave ballots), then every tile sums the counts before
+// it itself and writes its survivors in order — position k*256 + t is read by thread t, the
+// output offset of each wave's survivors comes from the ballots, so reads and writes stay
+// contiguous per wave (the generic scan reads and writes 16 consecutive items per lane).
+constexpr int kCompactTile = 4096;
+__global__ __launch_bounds__(256) void k_compact_count(const uint32_t* __restrict__ slots,
+                                                       uint32_t n, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t T0 = blockIdx.x * (uint32_t)kCompactTile;
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kCompactTile / 256; ++k) {
+    const uint32_t i = T0 + k * 256u + t;
+    c += (uint32_t)__popcll(__ballot(i < n && slots[i] != kInvalid));
+  }
+  if (lane == 0) wsum[wv] = c;
+  __syncthreads();
+  if (t == 0) counts[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restrict__ slots,
+                                                       uint32_t n,
+                                                       const uint32_t* __restrict__ counts,
+                                                       uint32_t* __restrict__ out,
+                                                       uint32_t* __restrict__ total) {
+  constexpr int K = kCompactTile / 256;
+  __shared__ uint32_t cnt[K * 4], pre[K * 4 + 1], wsum[4];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t T0 = blockIdx.x * (uint32_t)kCompactTile;
+  // survivors of the tiles before this one
+  uint32_t before = 0;
+  for (uint32_t j = t; j < blockIdx.x; j += 256) before += counts[j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+  if (lane == 0) wsum[wv] = before;
+  uint32_t v[K];
+  uint64_t m[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t i = T0 + k * 256u + t;
+    v[k] = i < n ? slots[i] : kInvalid;
+    m[k] = __ballot(v[k] != kInvalid);
+    if (lane == 0) cnt[k * 4 + wv] = (uint32_t)__popcll(m[k]);
+  }
+  __syncthreads();
+  if (t == 0) {  // offsets of the (row k, wave w) groups in position order
+    uint32_t a = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    for (int q = 0; q < K * 4; ++q) {
+      pre[q] = a;
+      a += cnt[q];
+    }
+    pre[K * 4] = a;
+  }
+  __syncthreads();
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (v[k] != kInvalid) out[pre[k * 4 + wv] + (uint32_t)__popcll(m[k] & below)] = v[k];
+  if (blockIdx.x == gridDim.x - 1 && t == 0) *total = pre[K * 4];
+}
+
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
                     Counters* ctr, hipStream_t s) {
-  device_scan(SrcLive{slots}, DstCompact{slots, out}, n, tile_sums, &ctr->total, &ctr->err, s);
+  if (scan_variant() == 2 || n == 0) {  // KLSH_SCAN=3k: the generic scan (A/B)
+    device_scan(SrcLive{slots}, DstCompact{slots, out}, n, tile_sums, &ctr->total, &ctr->err, s);
+    return;
+  }
+  const uint32_t ntiles = (n + kCompactTile - 1) / kCompactTile;
+  uint32_t* counts = tile_sums + kScanSumsWord;
+  k_compact_count<<<ntiles, 256, 0, s>>>(slots, n, counts);
+  k_compact_apply<<<ntiles, 256, 0, s>>>(slots, n, counts, out, &ctr->total);
 }
 
 // ========================================================================== radix sort ==========

@@ -381,6 +381,96 @@ __global__ __launch_bounds__(1024) void k_classify(const uint32_t* __restrict__ 
   if (cls >= 0) w.cls[cls][bbase[cls] + myoff] = make_uint2(p, b);
 }
 
+// Runs of equal keys found and classified in one pass (replaces the head-flag scan + k_classify):
+// a tile of 4096 positions is read coalesced (position k*256 + t by thread t), head flags become
+// a 4096-bit LDS bitmap (wave ballots), each head finds its run's end as the next set bit (the
+// last run of the tile looks past the tile end, one wave, 64 keys per step), and the runs go to
+// their class lists with one global atomic per class per workgroup.
+constexpr int kRunTile = 4096;
+__global__ __launch_bounds__(256) void k_runs(const uint32_t* __restrict__ key, uint32_t lo,
+                                              uint32_t n, int bucket_thr, MergeWork w,
+                                              Counters* ctr) {
+  __shared__ uint64_t hb[kRunTile / 64];  // head bitmap of the tile, word = 64 positions
+  __shared__ uint32_t bcnt[kGroupClasses + 1], bbase[kGroupClasses + 1];
+  __shared__ uint32_t s_tail_end;  // first head at or after the tile end (or n)
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t T0 = blockIdx.x * (uint32_t)kRunTile;
+  if (t <= (uint32_t)kGroupClasses) bcnt[t] = 0u;
+  const uint32_t* kp = key + lo;
+#pragma unroll
+  for (int k = 0; k < kRunTile / 256; ++k) {
+    const uint32_t i = T0 + k * 256u + t;
+    bool head = false;
+    if (i < n) head = i == 0 || kp[i] != kp[i - 1];
+    const uint64_t m = __ballot(head);
+    if (lane == 0) hb[k * 4 + wv] = m;
+  }
+  if (wv == 0) {  // the end of the tile's last run: the first head at or after T0 + kRunTile
+    uint32_t j = T0 + (uint32_t)kRunTile, end = n;
+    while (j < n) {
+      const uint32_t q = j + lane;
+      const bool h = q < n && kp[q] != kp[q - 1];
+      const uint64_t m = __ballot(h);
+      if (m) {
+        end = j + (uint32_t)__builtin_ctzll(m);
+        break;
+      }
+      j += 64u;
+    }
+    if (lane == 0) s_tail_end = min(end, n);
+  }
+  __syncthreads();
+  const uint32_t tail_end = s_tail_end;
+  uint32_t bl[kRunTile / 256];  // run length of the head at my position k*256 + t, 0 if none
+  int cl[kRunTile / 256];
+  uint32_t off[kRunTile / 256];
+  uint32_t heads = 0;
+#pragma unroll
+  for (int k = 0; k < kRunTile / 256; ++k) {
+    const uint32_t q = k * 256u + t;  // tile-local position
+    bl[k] = 0u;
+    cl[k] = -1;
+    off[k] = 0u;
+    if ((hb[q >> 6] >> (q & 63u)) & 1ull) {
+      uint32_t wi = q >> 6;
+      uint64_t m = hb[wi] & ~((2ull << (q & 63u)) - 1ull);  // heads after q in its word
+      while (!m && ++wi < (uint32_t)(kRunTile / 64)) m = hb[wi];
+      const uint32_t next = m ? T0 + wi * 64u + (uint32_t)__builtin_ctzll(m) : tail_end;
+      const uint32_t b = next - (T0 + q);
+      bl[k] = b;
+      ++heads;
+      if ((bucket_thr >= 0 && b > (uint32_t)bucket_thr) || b > 64u) {
+        queue_long_run(lo + T0 + q, b, bucket_thr, w, ctr);
+      } else if (b >= 2) {
+        cl[k] = size_class(b);
+        off[k] = atomicAdd(&bcnt[cl[k]], 1u);
+      }
+    }
+  }
+  // heads of the workgroup (statistics: ctr->n_seg = runs)
+  {
+    uint32_t hsum = heads;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hsum += __shfl_xor(hsum, o, 64);
+    if (lane == 0 && hsum) atomicAdd(&bcnt[kGroupClasses], hsum);
+  }
+  __syncthreads();
+  if (t < (uint32_t)kGroupClasses && bcnt[t]) bbase[t] = atomicAdd(&ctr->n_cls[t], bcnt[t]);
+  if (t == (uint32_t)kGroupClasses && bcnt[t]) atomicAdd(&ctr->n_seg, bcnt[t]);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kRunTile / 256; ++k)
+    if (cl[k] >= 0) w.cls[cl[k]][bbase[cl[k]] + off[k]] = make_uint2(lo + T0 + k * 256u + t, bl[k]);
+}
+
+static bool runs_via_scan() {  // KLSH_RUNS=scan: head-flag scan + k_classify (A/B)
+  static const bool v = [] {
+    const char* e = getenv("KLSH_RUNS");
+    return e && std::string(e) == "scan";
+  }();
+  return v;
+}
+
 // One wave per batch of 64/G runs of one size class (persistent over the class list).
 // One wave per batch of 64/G runs of one size class (persistent over the class list).  The list
 // entry and the slots of the NEXT batch are loaded while the current one is merged.
@@ -1455,16 +1545,17 @@ template <int D>
 static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
                           uint32_t* slots, const Decider& dc, const MergeWork& w, Counters* ctr,
                           uint32_t n, hipStream_t s) {
-  k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
+  if (runs_via_scan()) k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
   // Persistent grids: run counts live on the device; each grid strides over its list.
   auto grid = [&](int c, uint32_t per_wave) {
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
   const Fork f(w, s);
-  // longest walks first on each stream
+  // longest walks first on each stream; the longest runs (few, long walks) on the main stream,
+  // concurrent with the auxiliary ones (it waits for them at the join)
   launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(0));
-  launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, f.lane(0));
-  launch_huge(w, slots, dc, r, ctr, n, f.lane(0));
+  launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
+  launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   k_merge_group<64, D><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
   k_merge_group<32, D><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
@@ -1492,14 +1583,14 @@ static void launch_big_wide(const MergeWork& w, int c, uint32_t* slots, const De
 static void launch_groups_wide(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
                                uint32_t* slots, const Decider& dc, const MergeWork& w,
                                Counters* ctr, uint32_t n, hipStream_t s) {
-  k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
+  if (runs_via_scan()) k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
   auto grid = [&](int c, uint32_t per_wave) {
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
   const Fork f(w, s);
   launch_big_wide<384, 256, 32>(w, 1, slots, dc, r, ctr, n, f.lane(0));
-  launch_big_wide<896, 256, 16>(w, 2, slots, dc, r, ctr, n, f.lane(0));
-  launch_huge(w, slots, dc, r, ctr, n, f.lane(0));
+  launch_big_wide<896, 256, 16>(w, 2, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
+  launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   k_merge_group_wide<64><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
   k_merge_group_wide<32><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
@@ -1514,7 +1605,10 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   if (hi <= lo) return;
   const uint32_t n = hi - lo;
   const Decider dc = make_decider(thr);
-  device_scan(SrcHead{key, lo}, DstSegStart{w.seg, lo}, n, w.tile_sums, &ctr->n_seg, &ctr->err, s);
+  if (runs_via_scan())
+    device_scan(SrcHead{key, lo}, DstSegStart{w.seg, lo}, n, w.tile_sums, &ctr->n_seg, &ctr->err, s);
+  else
+    k_runs<<<(n + kRunTile - 1) / kRunTile, 256, 0, s>>>(key, lo, n, bucket_thr, w, ctr);
   switch (r.d) {
     case 8: launch_groups<8>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
     case 16: launch_groups<16>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;

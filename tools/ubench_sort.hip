@@ -39,7 +39,7 @@ int main(int argc, char** argv) {
   }
   uint32_t *k0, *v0, *k1, *v1, *ws, *ts, *kk, *vv;
   klsh::Counters* ctr;
-  const size_t wsw = klsh::sort_ws_words(n), tsw = (256ull * n) / klsh::kScanTile + 1024;
+  const size_t wsw = klsh::sort_ws_words(n), tsw = klsh::scan_ws_words(n);
   CK(hipMalloc(&k0, 4ull * n)); CK(hipMalloc(&v0, 4ull * n));
   CK(hipMalloc(&k1, 4ull * n)); CK(hipMalloc(&v1, 4ull * n));
   CK(hipMalloc(&kk, 4ull * n)); CK(hipMalloc(&vv, 4ull * n));
