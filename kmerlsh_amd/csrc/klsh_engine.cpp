@@ -143,6 +143,13 @@ struct klsh_ctx {
   size_t drec_cap = 0, drec_all_cap = 0;  // words
   uint64_t shard_cap = 0;
   double t_enqueued = 0.0;  // diagnostics (KLSH_ITER_LOG): host time when an iteration was queued
+  // KLSH_GRID_HINTS=1: size the big-run grids from the previous iteration's run counts.  Off by
+  // default: measured slower on C2 (346 -> 370 ms; with fewer pending big-run workgroups the
+  // small-run waves take the CUs the big runs need).
+  bool grid_hints = [] {
+    const char* e = getenv("KLSH_GRID_HINTS");
+    return e && e[0] == '1';
+  }();
 
   ~klsh_ctx() { release(); }
 
@@ -668,12 +675,28 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
                              klsh_stats* st, bool timed) {
   uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
   if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, st, timed)) return e;
+  // the next iteration's big-run grids: twice this iteration's run counts (plus slack)
+  uint32_t next_hint[klsh::kBigClasses + 1];
+  for (int c = 0; c < klsh::kBigClasses; ++c) next_hint[c] = 2 * ctx->h_ctr->n_big[c] + 4;
+  next_hint[klsh::kBigClasses] = 2 * ctx->h_ctr->n_huge + 2;
+  uint32_t small_batches = (ctx->h_ctr->n_cls[0] + 63) / 64;
+  for (int c = 1; c < klsh::kGroupClasses; ++c) {
+    const uint32_t per = 64u >> (c + 1);  // runs per batch: 64 / G, G = 2 << c
+    small_batches += (ctx->h_ctr->n_cls[c] + per - 1) / per;
+  }
+  const uint32_t next_small = std::max<uint32_t>(2 * small_batches + 64, 256);
   if (ctx->h_ctr->n_over > 0) {
     std::vector<uint2> over;
     uint64_t hyp = 0;
     if (int e = oversize_runs(ctx, &over, &hyp)) return e;
+    memset(ctx->mw.hint, 0, sizeof(ctx->mw.hint));  // nested regions: no history
+    ctx->mw.hint_small = 0;
     if (int e = merge_nested(ctx, fk, fv, n, thr, over, seed_base, rng_counter, out, st))
       return e;
+  }
+  if (ctx->grid_hints) {
+    memcpy(ctx->mw.hint, next_hint, sizeof(next_hint));
+    ctx->mw.hint_small = next_small;
   }
   if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
   ctx->n_live = ctx->h_ctr->total;
@@ -1040,6 +1063,8 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   const float sim_step = (max_similarity - min_similarity) / (float)iterations;
   float threshold = max_similarity;
 
+  memset(ctx->mw.hint, 0, sizeof(ctx->mw.hint));  // no run counts seen yet in this call
+  ctx->mw.hint_small = 0;
   // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
   // lshash.cc:36-42), so repeated timed calls never reuse a previous call's tables.
   ctx->w_count = 0;

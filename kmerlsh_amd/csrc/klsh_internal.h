@@ -70,6 +70,12 @@ struct MergeWork {
   // Size classes run concurrently on kMergeStreams auxiliary streams (fork after the run
   // classification, join before the compaction): in the late, small iterations each class kernel
   // is one long sequential walk, and serialised walks would add up.  aux[0] == nullptr: one stream.
+  // Grid hints for the big-run / huge-run kernels (0 = none: size for the worst case).  Their
+  // workgroups need most of a CU's LDS, so even empty ones wait for a free CU; the engine passes
+  // twice the previous iteration's run counts (the kernels loop over their lists, so any grid
+  // is correct).
+  uint32_t hint[kBigClasses + 1];
+  uint32_t hint_small;  // the same for the fused small-run kernel (batches)
   hipStream_t aux[3];
   hipEvent_t fork;
   hipEvent_t join[3];

@@ -381,6 +381,155 @@ __global__ __launch_bounds__(1024) void k_classify(const uint32_t* __restrict__ 
   if (cls >= 0) w.cls[cls][bbase[cls] + myoff] = make_uint2(p, b);
 }
 
+// ------------------------------------------------- all small-run classes in one launch -----
+// Runs of 2..64 rows of every size class in ONE persistent launch: the batches of all classes
+// (a batch = one wave's 64/G runs of class G; 64 runs of 2 for the pair class) are numbered in
+// one space, most expensive class first, and wave w takes batches w, w + grid, ...  Compared
+// with one kernel per class on three streams this removes the per-class launch chains and the
+// idle tails of the small classes.  The next batch's list entry and slot are loaded while the
+// current batch is merged.
+template <int G>
+__device__ __forceinline__ uint32_t batches_of(uint32_t n) {
+  return (n + (64u / G) - 1) / (64u / G);
+}
+
+template <int D>
+__device__ __forceinline__ void pair_batch(const uint2* __restrict__ list, uint32_t n, uint32_t bi,
+                                           uint32_t* __restrict__ slots, const Decider& dc,
+                                           const Rows& r, Counters* ctr, uint32_t* dlist) {
+  const uint32_t k = bi * 64u + __lane_id();
+  bool merged = false;
+  uint32_t s0 = 0;
+  if (k < n) {
+    const uint2 e = list[k];
+    s0 = slots[e.x];
+    const uint32_t s1 = slots[e.x + 1];
+    float x0[D], x1[D];
+    load_row<D>(r.x + (size_t)s0 * r.dp, x0);
+    load_row<D>(r.x + (size_t)s1 * r.dp, x1);
+    float dot = 0.0f;
+#pragma unroll
+    for (int q = 0; q < D; ++q) dot = dot + x1[q] * x0[q];  // cosine(c[1], c[0]), in order
+    const float n0 = r.nrm[s0], n1 = r.nrm[s1];
+    if (decide(dc, dot, __builtin_sqrtf(n1) * __builtin_sqrtf(n0))) {
+      merged = true;
+      const uint32_t ca = r.cnt[s1], cb = r.cnt[s0];  // current = row 1, candidate = row 0
+      const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+      float nn = 0.0f;
+      float* xo = r.x + (size_t)s0 * r.dp;
+#pragma unroll
+      for (int q = 0; q < D; q += 4) {
+        float4 v;
+        v.x = consensus(x1[q], fa, x0[q], fb, fn);
+        v.y = consensus(x1[q + 1], fa, x0[q + 1], fb, fn);
+        v.z = consensus(x1[q + 2], fa, x0[q + 2], fb, fn);
+        v.w = consensus(x1[q + 3], fa, x0[q + 3], fb, fn);
+        nn = nn + v.x * v.x;
+        nn = nn + v.y * v.y;
+        nn = nn + v.z * v.z;
+        nn = nn + v.w * v.w;
+        *reinterpret_cast<float4*>(xo + q) = v;
+      }
+      r.nrm[s0] = nn;
+      link_members(r, s1, s0);  // ids_current ++ ids_candidate; cnt[s1] = 0
+      slots[e.x + 1] = kInvalid;
+    }
+  }
+  if (dlist) append_slot(merged, s0, dlist, &ctr->n_delta);
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void k_merge_small(MergeWork w, uint32_t* __restrict__ slots,
+                                                    Decider dc, Rows r, Counters* ctr) {
+  __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
+  constexpr int NC = kGroupClasses;
+  uint32_t n[NC], nb[NC], start[NC + 1];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    n[c] = __hip_atomic_load(&ctr->n_cls[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  nb[0] = (n[0] + 63u) / 64u;
+  nb[1] = batches_of<4>(n[1]);
+  nb[2] = batches_of<8>(n[2]);
+  nb[3] = batches_of<16>(n[3]);
+  nb[4] = batches_of<32>(n[4]);
+  nb[5] = batches_of<64>(n[5]);
+  // batch space: class 5 (64-row runs) first ... class 0 (pairs) last
+  start[NC] = 0;
+  {
+    uint32_t a = 0;
+#pragma unroll
+    for (int c = NC - 1; c >= 0; --c) {
+      start[c] = a;
+      a += nb[c];
+    }
+    start[NC] = a;  // total
+  }
+  const uint32_t total = start[NC];
+  const uint32_t lane = threadIdx.x;
+  auto locate = [&](uint32_t t, int& c, uint32_t& bi) {
+    c = 0;
+#pragma unroll
+    for (int q = NC - 1; q >= 0; --q)
+      if (t >= start[q] && t < start[q] + nb[q]) c = q;
+    bi = t - start[c];
+  };
+  // the lane's (run, position) in batch bi of class c: entry and slot
+  auto fetch = [&](uint32_t t, uint2& e, uint32_t& slot) {
+    e = make_uint2(0u, 0u);
+    slot = 0u;
+    if (t >= total) return;
+    int c;
+    uint32_t bi;
+    locate(t, c, bi);
+    if (c == 0) return;  // pairs load their own
+    const uint32_t G = 2u << c, NG = 64u / G;
+    const uint32_t k = bi * NG + lane / G, g = lane & (G - 1);
+    if (k < n[c]) {
+      e = w.cls[c][k];
+      if (g < e.y) slot = slots[e.x + g];
+    }
+  };
+  float4 rb[1];
+  uint2 e;
+  uint32_t slot;
+  fetch(blockIdx.x, e, slot);
+  for (uint32_t t = blockIdx.x; t < total; t += gridDim.x) {
+    uint2 e_next;
+    uint32_t slot_next;
+    fetch(t + gridDim.x, e_next, slot_next);
+    int c;
+    uint32_t bi;
+    locate(t, c, bi);
+    auto none = [] {};
+    switch (c) {  // wave-uniform
+      case 0: pair_batch<D>(w.cls[0], n[0], bi, slots, dc, r, ctr, w.dlist); break;
+      case 1: merge_batch<4, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
+      case 2: merge_batch<8, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
+      case 3: merge_batch<16, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
+      case 4: merge_batch<32, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
+      default: merge_batch<64, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
+    }
+    e = e_next;
+    slot = slot_next;
+  }
+}
+
+static bool big384_rows_lds() {  // KLSH_BIG384_LDS=0: 129..384-row runs read rows from L2
+  static const bool v = [] {
+    const char* e = getenv("KLSH_BIG384_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+static bool small_fused() {  // KLSH_SMALL=split: one kernel per size class on the streams (A/B)
+  static const bool v = [] {
+    const char* e = getenv("KLSH_SMALL");
+    return !(e && std::string(e) == "split");
+  }();
+  return v;
+}
+
 // Runs of equal keys found and classified in one pass (replaces the head-flag scan + k_classify):
 // a tile of 4096 positions is read coalesced (position k*256 + t by thread t), head flags become
 // a 4096-bit LDS bitmap (wave ballots), each head finds its run's end as the next set bit (the
@@ -1137,7 +1286,8 @@ static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, 
                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
   }();
   (void)lds_ok;
-  const uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
+  uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
+  if (w.hint[kBigClasses]) g = std::min(g, w.hint[kBigClasses]);
   k_merge_huge<<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
 }
 
@@ -1507,7 +1657,8 @@ static void launch_big(const MergeWork& w, int c, uint32_t* slots, const Decider
   }();
   (void)lds_ok;
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
-  const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
+  uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
+  if (w.hint[c]) g = std::min(g, w.hint[c]);
   k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist);
 }
 
@@ -1553,10 +1704,21 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   const Fork f(w, s);
   // longest walks first on each stream; the longest runs (few, long walks) on the main stream,
   // concurrent with the auxiliary ones (it waits for them at the join)
-  launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(0));
+  if (big384_rows_lds())
+    launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(0));
+  else
+    launch_big<D, 384, 256, false>(w, 1, slots, dc, r, ctr, n, f.lane(0));
   launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
+  if (small_fused()) {
+    // a persistent grid: 2x the batches of the previous iteration (the kernel strides over its
+    // batches, so any grid is correct), at most what the GPU holds twice over
+    uint32_t g = 4608;
+    if (w.hint_small) g = std::min<uint32_t>(g, w.hint_small);
+    k_merge_small<D><<<g, 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
+    return;
+  }
   k_merge_group<64, D><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
   k_merge_group<32, D><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
   k_merge_group<16, D><<<grid(3, 4), 64, 0, f.lane(2)>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
@@ -1576,7 +1738,8 @@ static void launch_big_wide(const MergeWork& w, int c, uint32_t* slots, const De
   }();
   (void)lds_ok;
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
-  const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
+  uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
+  if (w.hint[c]) g = std::min(g, w.hint[c]);
   k_merge_big_wide<RB, NT, KC><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist);
 }
 

@@ -1,4 +1,4 @@
 cd $GRAFT_REPO_ROOT
-for e in "X=1" "KLSH_BIG_PRIORITY=0" "KLSH_RUNS=scan" "KLSH_SCAN=3k" "X=2"; do
+for e in "X=1" "KLSH_BIG384_LDS=0" "KLSH_SMALL=split" "KLSH_SMALL=split KLSH_BIG384_LDS=0" "X=2"; do
   env $e timeout -k 5 120 python bench.py --steps 3 --warmup 1 --cpu-baseline none 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$e', round(d['ms_per_step'],1), d['final_clusters'])"
 done
