@@ -311,21 +311,176 @@ __global__ __launch_bounds__(256) void k_project_generic(const float* __restrict
   keys[p] = key | key_or;
 }
 
+// Matrix-core projection, certified.  S = X W^T for 32 rows x 32 hyperplanes per wave with the
+// bf16x3 split (x = hi + lo; hi.hi + hi.lo + lo.hi, f32 accumulation) on v_mfma_f32_32x32x16_bf16.
+// |S - s| <= eps * |w| |x| against the reference's sequential f32 sum s (eps from
+// project_eps(d)), so every sign with |S| > eps |w| |x| is the reference's bit; the rest (about
+// 1e-3 of the row-hyperplane pairs, and any NaN or tiny row) take the exact sequential chain.
+// The row norms come from the loaded row itself (approximate, only a bound).  The sign bits of a
+// row across its hyperplanes come out of one wave ballot per accumulator register.
+typedef __bf16 pbf16x8 __attribute__((ext_vector_type(8)));
+typedef float pf32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void psplit8(float4 u, float4 v, pbf16x8& hi, pbf16x8& lo) {
+  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 hb = (__bf16)x[j];
+    hi[j] = hb;
+    lo[j] = (__bf16)(x[j] - (float)hb);  // exact in f32
+  }
+}
+
+float project_eps(int d) {
+  // 3 * 2^-16 (split residuals and the dropped lo.lo term) + (3d + 2) * 2^-23 (f32 accumulation of
+  // the 3d MFMA terms, counted at twice the unit roundoff) + d * 2^-23 (the reference's own sum),
+  // doubled for headroom
+  return 2.0f * (3.0f * 0x1p-16f + (float)(4 * d + 2) * 0x1p-23f);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_project_mfma(const float* __restrict__ X, int dp,
+                                                      const uint32_t* __restrict__ slots,
+                                                      uint32_t* __restrict__ keys, uint32_t n,
+                                                      const float* __restrict__ W, int h,
+                                                      uint32_t key_or, float eps) {
+  constexpr int ST = D + 4;
+  constexpr int KS = D / 16;  // k-steps of 16
+  __shared__ __attribute__((aligned(16))) float sw[32 * ST];  // hyperplane j at row j (0 if j >= h)
+  __shared__ float swn[32];                                    // |w_j| (a bound)
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, r = lane & 31u, hh = lane >> 5;
+  for (int i = (int)t; i < 32 * D; i += 256) {
+    const int j = i / D, k = i % D;
+    sw[j * ST + k] = j < h ? W[(size_t)j * dp + k] : 0.0f;
+  }
+  __syncthreads();
+  if (t < 32) {
+    float a = 0.0f;
+    for (int k = 0; k < D; ++k) a += sw[t * ST + k] * sw[t * ST + k];
+    swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;  // a bound: the hardware sqrt (1 ulp) suffices
+  }
+  __syncthreads();
+  // this lane's B fragments: hyperplane r, k = 16s + 8hh + e
+  pbf16x8 bh[KS], bl[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const float* wp = sw + r * ST + 16 * s + 8 * hh;
+    psplit8(*reinterpret_cast<const float4*>(wp), *reinterpret_cast<const float4*>(wp + 4), bh[s], bl[s]);
+  }
+  const float wn = swn[r];
+  const bool col_ok = (int)r < h;
+  // rows of the wave's next group are loaded while the current group is computed
+  const uint32_t step = gridDim.x * 128u;
+  uint32_t g0 = (blockIdx.x * 4u + wv) * 32u;
+  float4 xa[KS][2];
+  auto load_group = [&](uint32_t g) {
+    if (g >= n) return;
+    const uint32_t rw = g + r;
+    const float* xr = X + (size_t)slots[rw < n ? rw : g] * dp + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      xa[s][0] = *reinterpret_cast<const float4*>(xr + 16 * s);
+      xa[s][1] = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
+    }
+  };
+  load_group(g0);
+  for (; g0 < n; g0 += step) {
+    const uint32_t row = g0 + r;
+    const bool valid = row < n;
+    pbf16x8 ah[KS], al[KS];
+    float ss = 0.0f;  // this lane's half of |x|^2 (a bound only)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      psplit8(xa[s][0], xa[s][1], ah[s], al[s]);
+      ss += xa[s][0].x * xa[s][0].x + xa[s][0].y * xa[s][0].y + xa[s][0].z * xa[s][0].z +
+            xa[s][0].w * xa[s][0].w + xa[s][1].x * xa[s][1].x + xa[s][1].y * xa[s][1].y +
+            xa[s][1].z * xa[s][1].z + xa[s][1].w * xa[s][1].w;
+    }
+    load_group(g0 + step);
+    pf32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], bh[s], acc, 0, 0, 0);
+    }
+    ss += __shfl_xor(ss, 32, 64);
+    const float xn = __builtin_amdgcn_sqrtf(ss) * 1.001f;  // >= |x| of row g0 + r
+    // acc[i] = S[row (i&3) + 8(i>>2) + 4hh][hyperplane r]; lane L < 32 collects row g0 + L
+    uint32_t bits = 0u, amb = 0u;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t ri = (i & 3) + 8u * (i >> 2) + 4u * hh;
+      const float xni = __shfl(xn, (int)ri, 64);
+      const float sv = acc[i];
+      const float bound = eps * wn * xni;
+      const bool pos = col_ok && sv >= 0.0f;
+      // NaN, a tiny or huge row, or |S| within the bound: the exact chain decides
+      const bool am = col_ok && (!(__builtin_fabsf(sv) > bound) || !(xni >= 0x1p-60f) ||
+                                 !(xni <= 0x1p60f));
+      const uint64_t bp = __ballot(pos), ba = __ballot(am);
+      const uint32_t r0 = (i & 3) + 8u * (i >> 2);
+      if (lane == r0) {
+        bits = (uint32_t)bp;
+        amb = (uint32_t)ba;
+      }
+      if (lane == r0 + 4u) {
+        bits = (uint32_t)(bp >> 32);
+        amb = (uint32_t)(ba >> 32);
+      }
+    }
+    if (lane < 32 && valid) {
+      if (amb) {  // rare: the reference's sequential chains (hash/lshash.cc:44-51)
+        const float* x = X + (size_t)slots[row] * dp;
+        while (amb) {
+          const int j = __builtin_ctz(amb);
+          amb &= amb - 1u;
+          const float* w = sw + j * ST;
+          float sd = 0.0f;
+          for (int k = 0; k < D; ++k) sd = sd + w[k] * x[k];
+          bits = sd >= 0.0f ? (bits | (1u << j)) : (bits & ~(1u << j));
+        }
+      }
+      // hyperplane 0 is the key's most significant bit
+      keys[row] = (h > 0 ? (__builtin_bitreverse32(bits) >> (32 - h)) : 0u) | key_or;
+    }
+  }
+}
+
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
                     const float* W, int h, uint32_t key_or, hipStream_t s) {
   if (n == 0) return;
   const dim3 grid((n + 255) / 256), block(256);
-  // KLSH_PROJECT: "pk2" (default: packed f32, 8 chains, 1 row per lane) | "pk2r" (2 rows per
+  // KLSH_PROJECT: "pk2" (default: packed f32, 8 chains, 1 row per lane) | "mfma" (matrix cores,
+  // d in {16, 32, 64}) | "pk2r" (2 rows per
   // lane; 4 for wide rows) | "pk" (4 chains) | "scalar" | "staged".  Measured on C2/C5: the extra
   // rows per lane only add register pressure (the kernel is not LDS-read bound).
   static const int variant = [] {
     const char* e = getenv("KLSH_PROJECT");
     if (!e) return 1;
     const std::string v(e);
-    return v == "pk" ? 0 : v == "pk2r" ? 4 : v == "scalar" ? 2 : v == "staged" ? 3 : 1;
+    return v == "pk" ? 0 : v == "pk2r" ? 4 : v == "scalar" ? 2 : v == "staged" ? 3 : v == "pk2" ? 5 : v == "mfma" ? 6 : 1;
   }();
   const bool staged = variant == 3;
   const dim3 grid2((n + 511) / 512);
+  // the certified matrix-core kernel (KLSH_PROJECT=mfma): bit-exact, but at d <= 64 its
+  // per-pair epilogue (bound test + ballots) costs about what the packed chains cost — measured
+  // 161-167 vs 140-145 us per C2 launch — so the packed VALU kernel stays the default
+  if (variant == 6 && (r.d == 16 || r.d == 32 || r.d == 64)) {
+    const uint32_t groups = (n + 127) / 128;  // 4 waves x 32 rows per workgroup per step
+    static const uint32_t cap = [] {  // KLSH_PROJECT_GRID: persistent grid cap (A/B)
+      const char* e = getenv("KLSH_PROJECT_GRID");
+      return e ? (uint32_t)atoi(e) : 8192u;
+    }();
+    const dim3 gm(std::min<uint32_t>(groups, cap));
+    const float eps = project_eps(r.d);
+    if (r.d == 64) k_project_mfma<64><<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
+    else if (r.d == 32) k_project_mfma<32><<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
+    else k_project_mfma<16><<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
+    return;
+  }
   switch (r.d) {
 #define KLSH_PROJECT_CASE(DD)                                                                     \
   case DD:                                                                                      \
@@ -333,7 +488,7 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
       k_project_pk<DD, 2, 2><<<grid2, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);  \
     else if (variant == 0)                                                                      \
       k_project_pk<DD, 1, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);   \
-    else if (variant == 1)                                                                      \
+    else if (variant == 1 || variant == 5)                                                      \
       k_project_pk<DD, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);   \
     else if (staged)                                                                            \
       k_project<DD, true><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);      \

@@ -1716,7 +1716,13 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
     // batches, so any grid is correct), at most what the GPU holds twice over
     uint32_t g = 4608;
     if (w.hint_small) g = std::min<uint32_t>(g, w.hint_small);
-    k_merge_small<D><<<g, 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
+    // Large iterations: the small-run waves go after the 129..384-row runs on the same stream —
+    // run concurrently they take the CUs whose whole LDS those workgroups need, and starve them.
+    static const uint32_t serial_min = [] {  // KLSH_SERIAL_MIN: positions from which to serialise
+      const char* e = getenv("KLSH_SERIAL_MIN");
+      return e ? (uint32_t)strtoul(e, nullptr, 10) : 0xFFFFFFFFu;
+    }();
+    k_merge_small<D><<<g, 64, 0, n >= serial_min ? f.lane(0) : f.lane(2)>>>(w, slots, dc, r, ctr);
     return;
   }
   k_merge_group<64, D><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);

@@ -91,6 +91,58 @@ def test_hash_keys_random_vs_oracle(engine, oracle):
         assert np.array_equal(engine.hash_keys(rows, w), oracle.keys(rows, w)), (d, h)
 
 
+def test_hash_keys_close_calls_vs_oracle(engine, oracle):
+    """Rows on (or within float noise of) hyperplanes: the matrix-core screen cannot call these
+    signs, the exact sequential chain must (s == +0/-0 -> 1, tiny negative -> 0, NaN -> 0); plus
+    tiny, huge, zero and NaN rows."""
+    from kmerlsh_amd import _native
+
+    rng = np.random.default_rng(11)
+    for d, h in [(64, 23), (32, 18), (16, 9)]:
+        w, _ = _native.hyperplanes(7 + d, 0, h, d)
+        w64 = w.astype(np.float64)
+        rows = rng.normal(0, 1, size=(4000, d))
+        for i in range(0, 4000, 3):  # project out hyperplane i % h: s is rounding noise around 0
+            j = i % h
+            rows[i] -= (rows[i] @ w64[j]) / (w64[j] @ w64[j]) * w64[j]
+        rows = rows.astype(np.float32)
+        rows[1] = 0.0
+        rows[4] *= np.float32(1e-30)
+        rows[7] *= np.float32(1e30)
+        rows[10, 3] = np.nan
+        rows[13] = -0.0
+        got = engine.hash_keys(rows, w)
+        assert np.array_equal(got, oracle.keys(rows, w)), (d, h)
+
+
+def test_hash_keys_matrix_core_variant():
+    """The certified matrix-core projection (KLSH_PROJECT=mfma) on the same close calls, in a
+    child process (the kernel variant is chosen once per process)."""
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "import numpy as np, klsh_oracle as oracle\n"
+        "from kmerlsh_amd import _native\n"
+        "rng = np.random.default_rng(11)\n"
+        "with _native.Engine(0) as eng:\n"
+        "  for d, h in [(64, 23), (32, 31), (16, 9)]:\n"
+        "    w, _ = _native.hyperplanes(7 + d, 0, h, d)\n"
+        "    w64 = w.astype(np.float64)\n"
+        "    rows = rng.normal(0, 1, size=(5000, d))\n"
+        "    for i in range(0, 5000, 3):\n"
+        "      j = i %% h\n"
+        "      rows[i] -= (rows[i] @ w64[j]) / (w64[j] @ w64[j]) * w64[j]\n"
+        "    rows = rows.astype(np.float32)\n"
+        "    rows[1] = 0.0; rows[4] *= np.float32(1e-30); rows[7] *= np.float32(1e30)\n"
+        "    rows[10, 3] = np.nan; rows[13] = -0.0\n"
+        "    assert np.array_equal(eng.hash_keys(rows, w), oracle.keys(rows, w)), (d, h)\n"
+        "print('ok')\n"
+    ) % (ROOT, os.path.join(ROOT, "oracle"))
+    env = dict(os.environ, KLSH_PROJECT="mfma")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-2000:]
+
+
 # ------------------------------------------------------------------------------ p_cluster ---
 @pytest.mark.parametrize("name", ["pcluster_small", "pcluster_large", "pcluster_generic",
                                   "pcluster_d8"])

@@ -37,12 +37,16 @@ def test_target_is_gfx950(kernels):
 def test_projection_has_no_fused_multiply_add(kernels):
     proj = {k: v for k, v in kernels.items() if "k_project" in k}
     # d = 8, 16, 32, 64: scalar (direct, staged) and packed (4 chains, 8 chains with 1 or 2 rows
-    # per lane); packed wide-row kernels (1 and 4 rows per lane); the generic kernel
-    assert len(proj) == 23
+    # per lane); packed wide-row kernels (1 and 4 rows per lane); the generic kernel; the
+    # matrix-core kernels (d = 16, 32, 64)
+    assert len(proj) == 26
     for name, body in proj.items():
         bad = [ln.strip() for ln in body.splitlines() if FMA.match(ln)]
         assert not bad, (name, bad[:5])
-        if "_pk" in name:  # packed kernels: every product a separately rounded v_pk_mul_f32
+        if "mfma" in name:  # bf16x3 MFMA screen + the exact unfused chain for the close calls
+            assert "v_mfma_f32_32x32x16_bf16" in body, name
+            assert "v_mul_f32" in body and "v_add_f32" in body, name
+        elif "_pk" in name:  # packed kernels: every product a separately rounded v_pk_mul_f32
             assert body.count("v_pk_mul_f32") == body.count("v_pk_add_f32") > 0, name
         else:
             assert "v_mul_f32" in body or "v_pk_mul_f32" in body
