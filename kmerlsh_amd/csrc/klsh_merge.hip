@@ -55,10 +55,14 @@ __device__ unsigned long long g_mprof[8][8];
 #define MPROF_T() wall_clock64()
 #define MPROF_ADD(c, k, v) atomicAdd(&g_mprof[c][k], (unsigned long long)(v))
 #define MPROF_MAX(c, k, v) atomicMax(&g_mprof[c][k], (unsigned long long)(v))
+__device__ unsigned long long g_wprof[8][8];  // walk phases in shader clocks: find, select+
+                                              // consensus, dots, bits, steps, find rounds
+#define WPROF_CLK() __builtin_amdgcn_s_memtime()
 #else
 #define MPROF_T() 0ull
 #define MPROF_ADD(c, k, v) (void)0
 #define MPROF_MAX(c, k, v) (void)0
+#define WPROF_CLK() 0ull
 #endif
 
 __device__ __forceinline__ void lds_barrier() {
@@ -868,13 +872,38 @@ __device__ __forceinline__ float dot_acc_mem(float s, const float* a, const floa
   return s;
 }
 
+// The same sequential sum for a compile-time width D (a multiple of 4; D == 0: runtime d): every
+// load is issued before the chain starts, so the chain does not wait on a load every 4 terms.
+template <int D>
+__device__ __forceinline__ float dot_seq(const float* a, const float* b, int d) {
+  if constexpr (D == 0) {
+    return dot_acc_mem(0.0f, a, b, d);
+  } else {
+    float4 u[D / 4], v[D / 4];
+#pragma unroll
+    for (int k = 0; k < D / 4; ++k) {
+      u[k] = *reinterpret_cast<const float4*>(a + 4 * k);
+      v[k] = *reinterpret_cast<const float4*>(b + 4 * k);
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int k = 0; k < D / 4; ++k) {
+      s = s + u[k].x * v[k].x;
+      s = s + u[k].y * v[k].y;
+      s = s + u[k].z * v[k].z;
+      s = s + u[k].w * v[k].w;
+    }
+    return s;
+  }
+}
+
 // The walk of one 65..896-row run over its position-space decision matrix P (k_merge_big*),
 // shared by the whole workgroup: every step finds the first position q >= i whose row matches a
 // position below q (positions that find nothing change nothing), does the reference's merge
 // there, and recomputes the decisions of the rows still to be visited against the new row —
 // spread over all NT lanes (the new row's norm on one lane meanwhile).  Rows are read from
 // rowsL (LDS, stride ST) if given, else from memory; the new row is kept in LDS (cbuf).
-template <int RB, int NT, bool ROWS_LDS>
+template <int RB, int NT, bool ROWS_LDS, int D = 0>
 __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, uint32_t* slot,
                                          float* nrm, uint32_t* cnt, uint32_t* hd, uint32_t* tl,
                                          uint32_t* pos2row, float* sq, float* rowsL, int ST,
@@ -888,10 +917,13 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
     return ROWS_LDS ? rowsL + a * ST : r.x + (size_t)slot[a] * dp;
   };
   uint32_t i = 1, size = b, par = 0;
+  [[maybe_unused]] uint64_t wp[6] = {0, 0, 0, 0, 0, 0}, c0 = 0, c1 = 0;
   while (true) {
     // 1. the next position that merges
+    c0 = WPROF_CLK();
     uint32_t q = size;
     for (uint32_t q0 = i; q0 < size; q0 += NT) {
+      ++wp[5];
       const uint32_t qq = q0 + t;
       bool hit = false;
       if (qq < size) {
@@ -919,7 +951,11 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
         break;
       }
     }
+    c1 = WPROF_CLK();
+    wp[0] += c1 - c0;
+    c0 = c1;
     if (q >= size) break;
+    ++wp[4];
     i = q;
     // 2. its first matching position j < i (every wave computes it)
     const uint32_t rr = pos2row[i];
@@ -960,19 +996,25 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
     else __syncthreads();  // the new row in memory is visible to the workgroup
     --size;
     const uint32_t moved = size;  // old position of the row now at i
+    c1 = WPROF_CLK();
+    wp[1] += c1 - c0;
+    c0 = c1;
     // 4. dot products of the rows still to be visited with row c; row c's norm
     float dots[KP];
 #pragma unroll
     for (int kp = 0; kp < KP; ++kp) {
       const uint32_t qq = i + t + (uint32_t)kp * NT;
-      dots[kp] = qq < size ? dot_acc_mem(0.0f, rowp(pos2row[qq]), lc, d) : 0.0f;
+      dots[kp] = qq < size ? dot_seq<D>(rowp(pos2row[qq]), lc, d) : 0.0f;
     }
     if (t == NT - 1) {
-      const float nn = dot_acc_mem(0.0f, lc, lc, d);  // distance.cc:33-34
+      const float nn = dot_seq<D>(lc, lc, d);  // distance.cc:33-34
       nrm[c] = nn;
       sq[c] = __builtin_sqrtf(nn);
     }
     lds_barrier();
+    c1 = WPROF_CLK();
+    wp[2] += c1 - c0;
+    c0 = c1;
     // 5. position-space bits: the moved row's bit goes to position i, bit j is re-decided
     const float sc = sq[c];
 #pragma unroll
@@ -989,7 +1031,15 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
       }
     }
     lds_barrier();
+    c1 = WPROF_CLK();
+    wp[3] += c1 - c0;
   }
+#ifdef KLSH_MERGE_PROF
+  if (t == 0) {
+    const int cls = RB <= 128 ? 0 : RB <= 384 ? 1 : 2;
+    for (int k = 0; k < 6; ++k) atomicAdd(&g_wprof[cls][k], (unsigned long long)wp[k]);
+  }
+#endif
   // write back: survivors in position order, kInvalid after; rewritten rows; metadata
   for (uint32_t q = t; q < b; q += NT) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
   if (ROWS_LDS) {  // a survivor was rewritten iff its count rose (the global count is still old)
@@ -1150,7 +1200,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
     }
     __syncthreads();
     [[maybe_unused]] const uint64_t pt1 = MPROF_T();
-    big_walk<RB, NT, ROWS_LDS>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq,
+    big_walk<RB, NT, ROWS_LDS, D>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq,
                                ROWS_LDS ? rows : nullptr, ST, rows, wbuf, r, dc, slots, dlist, ctr);
     __syncthreads();
 #ifdef KLSH_MERGE_PROF
@@ -1178,6 +1228,7 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
 constexpr int kHugeNT = 512;
 constexpr uint32_t kHugeLdsRows = 8192;
 
+template <int D>  // D: d at compile time (unrolled dots), 0 = any d
 __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict__ list,
                                                        const uint32_t* count_ptr,
                                                        uint32_t* __restrict__ slots, Decider dc,
@@ -1220,7 +1271,7 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
         bool ok = false;
         if (j < i) {
           const uint32_t sj = S[j];
-          ok = decide(dc, dot_acc_mem(0.0f, xi, r.x + (size_t)sj * dp, d), sqi * sqrt_at(j));
+          ok = decide(dc, dot_seq<D>(xi, r.x + (size_t)sj * dp, d), sqi * sqrt_at(j));
         }
         const uint64_t m = __ballot(ok);
         if (lane == 0)
@@ -1252,7 +1303,7 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
       }
       __syncthreads();  // the new row is in memory and in LDS
       if (t == 0) {
-        const float nn = dot_acc_mem(0.0f, xi, xi, d);  // distance.cc:33-34
+        const float nn = dot_seq<D>(xi, xi, d);  // distance.cc:33-34
         r.nrm[sj] = nn;
         if (in_lds) lq[found] = __builtin_sqrtf(nn);
         link_members(r, si, sj);
@@ -1282,13 +1333,26 @@ static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, 
                         Counters* ctr, uint32_t n, hipStream_t s) {
   const size_t lds = sizeof(uint32_t) * kHugeLdsRows * 2 + sizeof(float) * (size_t)r.dp;
   static const bool lds_ok = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_huge),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
+    bool ok = true;
+    for (const void* f : {reinterpret_cast<const void*>(&k_merge_huge<0>),
+                          reinterpret_cast<const void*>(&k_merge_huge<8>),
+                          reinterpret_cast<const void*>(&k_merge_huge<16>),
+                          reinterpret_cast<const void*>(&k_merge_huge<32>),
+                          reinterpret_cast<const void*>(&k_merge_huge<64>)})
+      ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) ==
+                     hipSuccess;
+    return ok;
   }();
   (void)lds_ok;
   uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
   if (w.hint[kBigClasses]) g = std::min(g, w.hint[kBigClasses]);
-  k_merge_huge<<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
+  switch (r.d) {
+    case 8: k_merge_huge<8><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr); break;
+    case 16: k_merge_huge<16><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr); break;
+    case 32: k_merge_huge<32><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr); break;
+    case 64: k_merge_huge<64><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr); break;
+    default: k_merge_huge<0><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
+  }
 }
 
 // ------------------------------------------------------------------ wide rows (any d) -----
@@ -1800,8 +1864,18 @@ void merge_prof_dump(FILE* f) {
                  "  (per run %7.2f + %7.2f us)  max run %8.2f us  max b %llu\n",
               names[c], h[c][0], h[c][1], h[c][2], h[c][3] * 1e-5, h[c][4] * 1e-5,
               h[c][3] * 1e-2 / h[c][0], h[c][4] * 1e-2 / h[c][0], h[c][5] * 1e-2, h[c][6]);
+  unsigned long long wpf[8][8];
+  if (hipMemcpyFromSymbol(wpf, HIP_SYMBOL(g_wprof), sizeof(wpf)) == hipSuccess)
+    for (int c = 0; c < 3; ++c)
+      if (wpf[c][4])
+        fprintf(f, "[wprof] %-7s steps %9llu  clocks/step: find %7.0f  select+consensus %7.0f"
+                   "  dots %7.0f  bits %7.0f   find rounds/step %.2f\n",
+                names[c], wpf[c][4], (double)wpf[c][0] / wpf[c][4], (double)wpf[c][1] / wpf[c][4],
+                (double)wpf[c][2] / wpf[c][4], (double)wpf[c][3] / wpf[c][4],
+                (double)wpf[c][5] / wpf[c][4]);
   unsigned long long z[8][8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mprof), z, sizeof(z));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), z, sizeof(z));
 #else
   (void)f;
 #endif
