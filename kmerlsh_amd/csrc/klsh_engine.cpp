@@ -697,6 +697,12 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
   if (ctx->grid_hints) {
     memcpy(ctx->mw.hint, next_hint, sizeof(next_hint));
     ctx->mw.hint_small = next_small;
+  } else {
+    // always for the two rarest, most LDS-hungry classes (>384 rows: 142 KB, >896 rows: 64+ KB
+    // per workgroup): sized for the worst case, their mostly empty workgroups queue for whole CUs
+    // behind the other merge kernels and hold up the join (C2: 205 us per empty k_merge_huge)
+    ctx->mw.hint[2] = next_hint[2];
+    ctx->mw.hint[klsh::kBigClasses] = next_hint[klsh::kBigClasses];
   }
   if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
   ctx->n_live = ctx->h_ctr->total;

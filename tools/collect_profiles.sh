@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round profiles on the GPU box (run through gpurun from the repo root):
+#   C2 bench line, rocprofv3 kernel stats of one C2 step, FETCH_SIZE / WRITE_SIZE of the projection
+#   (separate --pmc passes), kernel stats of C4 and C5.  Outputs under gpurun_out/prof/.
+#   tools/collect_profiles.sh [c2|all]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+out=gpurun_out/prof
+mkdir -p $out
+set -o pipefail
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name"
+  timeout -k 10 "$secs" "$@" > $out/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+}
+run c2_bench 300 python bench.py --steps 3 --warmup 1
+run c2_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c2_stats -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline none
+run c2_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex k_project -d $out/c2_fetch -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline none
+run c2_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex k_project -d $out/c2_write -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline none
+if [ "$1" = all ]; then
+  run c4_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c4_stats -o run -- python bench.py --config c4 --steps 1 --warmup 0 --cpu-baseline none
+  run c5_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c5_stats -o run -- python bench.py --config c5 --steps 1 --warmup 0 --cpu-baseline none
+fi
+exit 0

@@ -1,4 +1,4 @@
 cd $GRAFT_REPO_ROOT
-export KLSH_MERGE_PROF=1
-KLSH_LIB=$PWD/kmerlsh_amd/lib_ab/libklsh_prof.so timeout -k 5 120 python bench.py --steps 1 --warmup 0 --iterations 1 --cpu-baseline none 2>&1 | grep -E "prof|timed"
-KLSH_LIB=$PWD/kmerlsh_amd/lib_ab/libklsh_prof.so timeout -k 5 120 python bench.py --steps 1 --warmup 0 --cpu-baseline none 2>&1 | grep -E "prof|timed"
+for e in "X=1" "KLSH_GRID_HINTS=1" "X=2"; do
+  env $e timeout -k 5 120 python bench.py --steps 3 --warmup 1 --cpu-baseline none 2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$e', round(d['ms_per_step'],1), d['final_clusters'])"
+done
