@@ -114,6 +114,7 @@ struct klsh_ctx {
   uint32_t* hist = nullptr;
   uint32_t* tile_sums = nullptr;
   klsh::MergeWork mw{};
+  klsh::ProjectWork pw{};     // wide-row matrix-core projection: fix-up list
   Counters* ctr = nullptr;
   Counters* h_ctr = nullptr;  // pinned
   float* W = nullptr;         // hyperplane pool on the device, [k - w_k0][dp]
@@ -223,6 +224,9 @@ struct klsh_ctx {
     dfree(rows.nxt); dfree(order); dfree(alt); dfree(keys); dfree(keys2); dfree(nk1);
     dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.seg); dfree(mw.over);
     dfree(mw.huge);
+    dfree(pw.fix);
+    dfree(pw.ws);
+    pw.cap = 0;
     for (auto& c : mw.big) dfree(c);
     for (auto& c : mw.cls) dfree(c);
     cap_slots = cap_members = 0;
@@ -281,6 +285,7 @@ struct klsh_ctx {
         (e = dalloc(&hist, klsh::sort_ws_words(s))) ||
         (e = dalloc(&tile_sums, klsh::scan_ws_words(s))) ||
         (e = dalloc(&mw.seg, s + 64)) || (e = dalloc(&mw.over, s + 64)) ||
+        (e = dalloc(&pw.fix, s)) || (e = dalloc(&pw.ws, 64)) ||
         (e = dalloc(&mw.big[0], s / 65 + 64)) || (e = dalloc(&mw.big[1], s / 129 + 64)) ||
         (e = dalloc(&mw.big[2], s / 385 + 64)) || (e = dalloc(&mw.huge, s / 897 + 64))) {
       release_state();
@@ -294,7 +299,9 @@ struct klsh_ctx {
     }
     // the look-back workspaces start zeroed (tickets, done counters, epochs, histograms) and the
     // kernels return them to zero; they are never cleared again
-    if (hipMemset(hist, 0, sizeof(uint32_t) * klsh::sort_ws_words(s)) != hipSuccess ||
+    pw.cap = (uint32_t)s;
+    if (hipMemset(pw.ws, 0, sizeof(uint32_t) * 64) != hipSuccess ||
+        hipMemset(hist, 0, sizeof(uint32_t) * klsh::sort_ws_words(s)) != hipSuccess ||
         hipMemset(tile_sums, 0, sizeof(uint32_t) * klsh::scan_ws_words(s)) != hipSuccess) {
       release_state();
       return fail(KLSH_E_HIP, "workspace init");
@@ -650,7 +657,8 @@ static int merge_nested(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, f
     // Sub-keys carry bit 31 (main keys are < 2^h <= 2^31, so never have it) and a bit 30 that
     // alternates between consecutive oversize regions, so no run crosses a region boundary.
     const uint32_t key_or = 0x80000000u | ((oi & 1u) << 30);
-    klsh::launch_project(ctx->rows, fv + p, ctx->nk1, b, ctx->hyperplane_ptr(k), h2, key_or, s);
+    klsh::launch_project(ctx->rows, fv + p, ctx->nk1, b, ctx->hyperplane_ptr(k), h2, key_or, s,
+                         &ctx->pw);
     uint32_t *rk = nullptr, *rv = nullptr;
     klsh::radix_sort(ctx->nk1, fv + p, ctx->nk2, ctx->nv2, b, h2, ctx->hist, ctx->tile_sums,
                      ctx->ctr, &rk, &rv, s);
@@ -737,7 +745,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
     KLSH_HIP(hipEventRecord(ctx->ev[0], s));
     klsh::launch_project(ctx->rows, ctx->order, ctx->keys, (uint32_t)n, ctx->hyperplane_ptr(k), h,
-                         0u, s);
+                         0u, s, &ctx->pw);
     KLSH_HIP(hipGetLastError());
     KLSH_HIP(hipEventRecord(ctx->ev[1], s));
     uint32_t *fk = nullptr, *fv = nullptr;
@@ -885,7 +893,8 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
     // 1. keys of my rows, key-range ownership, send counts
     KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
     KLSH_HIP(hipEventRecord(ctx->ev[0], s));
-    klsh::launch_project(ctx->rows, ctx->order, ctx->keys, n_g, ctx->hyperplane_ptr(k), h, 0u, s);
+    klsh::launch_project(ctx->rows, ctx->order, ctx->keys, n_g, ctx->hyperplane_ptr(k), h, 0u, s,
+                         &ctx->pw);
     KLSH_HIP(hipGetLastError());
     KLSH_HIP(hipEventRecord(ctx->ev[1], s));
     const int B = std::min(h, klsh::kMaxBinBits);
@@ -1218,12 +1227,15 @@ int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const fl
   r.dp = dp;
   uint32_t *slots = nullptr, *dkeys = nullptr;
   float* W = nullptr;
+  klsh::ProjectWork pw{};
   int e = 0;
   if ((e = dalloc(&r.x, n * dp)) || (e = dalloc(&slots, n)) || (e = dalloc(&dkeys, n)) ||
-      (e = dalloc(&W, (uint64_t)std::max(h, 1) * dp))) {
-    dfree(r.x); dfree(slots); dfree(dkeys); dfree(W);
+      (e = dalloc(&W, (uint64_t)std::max(h, 1) * dp)) || (e = dalloc(&pw.fix, n)) ||
+      (e = dalloc(&pw.ws, 64))) {
+    dfree(r.x); dfree(slots); dfree(dkeys); dfree(W); dfree(pw.fix); dfree(pw.ws);
     return e;
   }
+  pw.cap = (uint32_t)n;
   hipStream_t s = ctx->stream;
   std::vector<uint32_t> iota(n);
   for (uint64_t i = 0; i < n; ++i) iota[i] = (uint32_t)i;
@@ -1231,19 +1243,20 @@ int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const fl
   if (hipMemsetAsync(r.x, 0, sizeof(float) * n * dp, s) != hipSuccess ||
       hipMemcpy2DAsync(r.x, 4 * dp, rows, 4 * d, 4 * d, n, hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemsetAsync(W, 0, sizeof(float) * std::max(h, 1) * dp, s) != hipSuccess ||
+      hipMemsetAsync(pw.ws, 0, sizeof(uint32_t) * 64, s) != hipSuccess ||
       (h > 0 && hipMemcpy2DAsync(W, 4 * dp, table, 4 * d, 4 * d, h, hipMemcpyHostToDevice, s) !=
                     hipSuccess) ||
       hipMemcpyAsync(slots, iota.data(), 4 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
     rc = fail(KLSH_E_HIP, "upload");
   } else {
-    klsh::launch_project(r, slots, dkeys, (uint32_t)n, W, h, 0u, s);
+    klsh::launch_project(r, slots, dkeys, (uint32_t)n, W, h, 0u, s, &pw);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(keys, dkeys, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
       rc = fail(KLSH_E_HIP, "projection");
   }
   (void)hipStreamSynchronize(s);
-  dfree(r.x); dfree(slots); dfree(dkeys); dfree(W);
+  dfree(r.x); dfree(slots); dfree(dkeys); dfree(W); dfree(pw.fix); dfree(pw.ws);
   return rc;
 }
 

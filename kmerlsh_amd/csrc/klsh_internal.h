@@ -109,16 +109,28 @@ struct Decider {
   uint32_t fast;
   float g_lo, g_hi;
 };
-// |G - dot| <= 6.3e-5 * |a| |b| for the bf16x3 Gram value (hi/lo split, 3 MFMAs, f32
-// accumulation of 3d terms, d <= 64) against the reference's sequential f32 dot; the margin adds
-// headroom for den's rounding and the approximate quotient.
-constexpr float kGramMargin = 1.5e-4f;
+// |G - dot| <= 5.4e-5 * |a| |b| for the bf16x3 Gram value at d <= 64 (split residuals
+// 3.03 * 2^-16, the MFMA sum <= 29 chained f32 adds per term at 2u, the reference's own 65u; see
+// project_eps) against the reference's sequential f32 dot; the margin adds headroom for den's
+// rounding and the approximate quotient.
+constexpr float kGramMargin = 1.0e-4f;
 Decider make_decider(float thr);
+
+// Workspace of the wide-row matrix-core projection: the (row, hyperplane) pairs its screen could
+// not call (fix[0 .. cap)), a counter and a done counter (ws[0], ws[1]) that the fix-up kernel
+// returns to zero.  Zeroed once at allocation.
+struct ProjectWork {
+  uint2* fix;
+  uint32_t* ws;
+  uint32_t cap;
+};
 
 // ---- launch wrappers (all asynchronous on `s`) ------------------------------------------------
 // keys[p] = sign-hash of row slots[p] against h hyperplanes W (h x dp), OR'ed with key_or.
+// pw (may be null): the workspace that enables the matrix-core kernel for wide rows (d > 64).
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
-                    const float* W, int h, uint32_t key_or, hipStream_t s);
+                    const float* W, int h, uint32_t key_or, hipStream_t s,
+                    const ProjectWork* pw = nullptr);
 
 // Stable LSD radix sort of (keys, vals)[0..n) on the low `bits` bits. Uses ping-pong buffers;
 // returns via *out_k/*out_v which pair holds the result (one of (k0,v0) or (k1,v1)).

@@ -332,10 +332,13 @@ __device__ __forceinline__ void psplit8(float4 u, float4 v, pbf16x8& hi, pbf16x8
 }
 
 float project_eps(int d) {
-  // 3 * 2^-16 (split residuals and the dropped lo.lo term) + (3d + 2) * 2^-23 (f32 accumulation of
-  // the 3d MFMA terms, counted at twice the unit roundoff) + d * 2^-23 (the reference's own sum),
-  // doubled for headroom
-  return 2.0f * (3.0f * 0x1p-16f + (float)(4 * d + 2) * 0x1p-23f);
+  // |S - s| / (|w| |x|) <= 3.03 * 2^-16          split residuals and the dropped lo.lo term
+  //                      + (16 + 3 ceil(d/16) + 1) * 2^-23   the MFMA sum: each term passes through
+  //                        at most 16 internal adds + one per chained MFMA (counted at 2u)
+  //                      + (d + 1) * 2^-24        the reference's own sequential sum
+  // times 1.5 for headroom
+  const float ks = (float)((d + 15) / 16);
+  return 1.5f * (3.03f * 0x1p-16f + (17.0f + 3.0f * ks) * 0x1p-23f + (float)(d + 1) * 0x1p-24f);
 }
 
 template <int D>
@@ -449,8 +452,186 @@ __global__ __launch_bounds__(256) void k_project_mfma(const float* __restrict__ 
   }
 }
 
+// Wide rows (d > 64, any d): the same certified matrix-core screen with the hyperplanes pre-split
+// into bf16 hi/lo fragments in LDS ([k-step][lane] 32 B each: 64 KB at d = 512) and the row
+// streamed 64 columns at a time (8 loads in flight per lane).  The pairs the screen cannot call
+// (≈1 % at d = 512: the bound grows with d) go to a list that k_project_fix settles with the exact
+// sequential chains afterwards, one lane per pair — in-wave they would stall 31 other rows.
+__global__ __launch_bounds__(256) void k_project_mfma_wide(const float* __restrict__ X, int d, int dp,
+                                                           const uint32_t* __restrict__ slots,
+                                                           uint32_t* __restrict__ keys, uint32_t n,
+                                                           const float* __restrict__ W, int h,
+                                                           uint32_t key_or, float eps, ProjectWork pw) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+  const int KS = (d + 15) / 16;
+  pbf16x8* bfr = reinterpret_cast<pbf16x8*>(psm);  // [KS][64 lanes][hi, lo]
+  float* swn = reinterpret_cast<float*>(psm + (size_t)KS * 64 * 2 * sizeof(pbf16x8));  // [32]
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, r = lane & 31u, hh = lane >> 5;
+  // hyperplane fragments: entry (s, L) = W[j = L&31][16s + 8(L>>5) + 0..7], split
+  for (int e = (int)t; e < KS * 64; e += 256) {
+    const int sk = e >> 6, L = e & 63, j = L & 31, k0 = 16 * sk + 8 * (L >> 5);
+    float x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = (j < h && k0 + q < d) ? W[(size_t)j * dp + k0 + q] : 0.0f;
+    pbf16x8 hi, lo;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const __bf16 hb = (__bf16)x[q];
+      hi[q] = hb;
+      lo[q] = (__bf16)(x[q] - (float)hb);
+    }
+    bfr[2 * e] = hi;
+    bfr[2 * e + 1] = lo;
+  }
+  if (t < 32) {
+    float a = 0.0f;
+    for (int k = 0; k < d; ++k) {
+      const float v = (int)t < h ? W[(size_t)t * dp + k] : 0.0f;
+      a += v * v;
+    }
+    swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;
+  }
+  __syncthreads();
+  const float wn = swn[r];
+  const bool col_ok = (int)r < h;
+  const uint32_t step = gridDim.x * 128u;
+  for (uint32_t g0 = (blockIdx.x * 4u + wv) * 32u; g0 < n; g0 += step) {
+    const uint32_t row = g0 + r;
+    const bool valid = row < n;
+    const float* xr = X + (size_t)slots[valid ? row : g0] * dp;
+    pf32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    float ss = 0.0f;
+    // 4 k-steps (64 columns) per round; the next round's loads are issued before this round's math
+    float4 xa[4][2], xn4[4][2];
+    auto load_round = [&](int s0, float4 (&dst)[4][2]) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k0 = 16 * (s0 + q) + 8 * (int)hh;
+        dst[q][0] = k0 + 4 <= dp ? *reinterpret_cast<const float4*>(xr + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        dst[q][1] = k0 + 8 <= dp ? *reinterpret_cast<const float4*>(xr + k0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    };
+    load_round(0, xa);
+    for (int s0 = 0; s0 < KS; s0 += 4) {
+      if (s0 + 4 < KS) load_round(s0 + 4, xn4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (s0 + q < KS) {  // wave-uniform
+          pbf16x8 ah, al;
+          psplit8(xa[q][0], xa[q][1], ah, al);
+          ss += xa[q][0].x * xa[q][0].x + xa[q][0].y * xa[q][0].y + xa[q][0].z * xa[q][0].z +
+                xa[q][0].w * xa[q][0].w + xa[q][1].x * xa[q][1].x + xa[q][1].y * xa[q][1].y +
+                xa[q][1].z * xa[q][1].z + xa[q][1].w * xa[q][1].w;
+          const pbf16x8 bh = bfr[2 * ((s0 + q) * 64 + lane)], bl = bfr[2 * ((s0 + q) * 64 + lane) + 1];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        xa[q][0] = xn4[q][0];
+        xa[q][1] = xn4[q][1];
+      }
+    }
+    ss += __shfl_xor(ss, 32, 64);
+    const float xn = __builtin_amdgcn_sqrtf(ss) * 1.001f;
+    uint32_t bits = 0u, amb = 0u;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t ri = (i & 3) + 8u * (i >> 2) + 4u * hh;
+      const float xni = __shfl(xn, (int)ri, 64);
+      const float sv = acc[i];
+      const bool pos = col_ok && sv >= 0.0f;
+      const bool am = col_ok && (!(__builtin_fabsf(sv) > eps * wn * xni) || !(xni >= 0x1p-60f) ||
+                                 !(xni <= 0x1p60f));
+      const uint64_t bp = __ballot(pos), ba = __ballot(am);
+      const uint32_t r0 = (i & 3) + 8u * (i >> 2);
+      if (lane == r0) {
+        bits = (uint32_t)bp;
+        amb = (uint32_t)ba;
+      }
+      if (lane == r0 + 4u) {
+        bits = (uint32_t)(bp >> 32);
+        amb = (uint32_t)(ba >> 32);
+      }
+    }
+    if (lane < 32 && valid) {
+      keys[row] = (h > 0 ? (__builtin_bitreverse32(bits) >> (32 - h)) : 0u) | key_or;
+      if (amb) {  // to the fix-up list (the exact chains; in place if the list is full)
+        const uint32_t c = (uint32_t)__popc(amb);
+        const uint32_t at = atomicAdd(&pw.ws[0], c);
+        uint32_t a = amb, k = 0;
+        while (a) {
+          const int j = __builtin_ctz(a);
+          a &= a - 1u;
+          if (at + k < pw.cap) {
+            pw.fix[at + k] = make_uint2(row, (uint32_t)j);
+          } else {
+            const float* x = X + (size_t)slots[row] * dp;
+            const float* w = W + (size_t)j * dp;
+            float sd = 0.0f;
+            for (int q = 0; q < d; ++q) sd = sd + w[q] * x[q];
+            const uint32_t bit = 1u << (h - 1 - j);
+            keys[row] = sd >= 0.0f ? (keys[row] | bit) : (keys[row] & ~bit);
+          }
+          ++k;
+        }
+      }
+    }
+  }
+}
+
+// The exact sequential chain (hash/lshash.cc:44-51) of each listed (row, hyperplane) pair; the
+// key bit is set or cleared atomically (several pairs may share a row).  Persistent grid; the last
+// workgroup returns the list counters to zero.
+__global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X, int d, int dp,
+                                                     const uint32_t* __restrict__ slots,
+                                                     uint32_t* __restrict__ keys,
+                                                     const float* __restrict__ W, int h,
+                                                     ProjectWork pw) {
+  extern __shared__ __attribute__((aligned(16))) float fw[];  // the h hyperplanes, stride dp
+  __shared__ uint32_t s_last;
+  const uint32_t count = min(pw.ws[0], pw.cap);
+  if (blockIdx.x * 256u < count)
+    for (int i = (int)threadIdx.x; i < h * dp; i += 256) fw[i] = W[i];
+  __syncthreads();
+  for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < count; e += gridDim.x * 256u) {
+    const uint2 f = pw.fix[e];
+    const float* x = X + (size_t)slots[f.x] * dp;
+    const float* w = fw + (size_t)f.y * dp;
+    float sd = 0.0f;
+    int k = 0;
+    for (; k + 64 <= d; k += 64) {  // 64 columns per round, the row's loads issued first
+      float4 u[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) u[q] = *reinterpret_cast<const float4*>(x + k + 4 * q);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(w + k + 4 * q);
+        sd = sd + v.x * u[q].x;
+        sd = sd + v.y * u[q].y;
+        sd = sd + v.z * u[q].z;
+        sd = sd + v.w * u[q].w;
+      }
+    }
+    for (; k < d; ++k) sd = sd + w[k] * x[k];
+    const uint32_t bit = 1u << (h - 1 - (int)f.y);
+    if (sd >= 0.0f) atomicOr(&keys[f.x], bit);
+    else atomicAnd(&keys[f.x], ~bit);
+  }
+  if (threadIdx.x == 0) s_last = atomicAdd(&pw.ws[1], 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {
+    atomicExch(&pw.ws[0], 0u);
+    atomicExch(&pw.ws[1], 0u);
+  }
+}
+
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
-                    const float* W, int h, uint32_t key_or, hipStream_t s) {
+                    const float* W, int h, uint32_t key_or, hipStream_t s, const ProjectWork* pw) {
   if (n == 0) return;
   const dim3 grid((n + 255) / 256), block(256);
   // KLSH_PROJECT: "pk2" (default: packed f32, 8 chains, 1 row per lane) | "mfma" (matrix cores,
@@ -465,6 +646,26 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
   }();
   const bool staged = variant == 3;
   const dim3 grid2((n + 511) / 512);
+  // wide rows: the matrix-core kernel + exact fix-ups (default when the workspace is given;
+  // KLSH_PROJECT=pk2 keeps the packed VALU kernel)
+  if (pw && r.d > 64 && h > 0 && (variant == 1 || variant == 6)) {
+    const size_t lds = (size_t)((r.d + 15) / 16) * 64 * 2 * 16 + 32 * sizeof(float);
+    const size_t flds = sizeof(float) * (size_t)h * r.dp;  // the fix-up kernel's hyperplanes
+    if (lds <= 96 * 1024 && flds <= 128 * 1024) {
+      static const bool lds_ok =
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_mfma_wide),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_fix),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) == hipSuccess;
+      (void)lds_ok;
+      const uint32_t groups = (n + 127) / 128;
+      const dim3 gm(std::min<uint32_t>(groups, 2048u));
+      k_project_mfma_wide<<<gm, block, lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or,
+                                                 project_eps(r.d), *pw);
+      k_project_fix<<<1024, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw);
+      return;
+    }
+  }
   // the certified matrix-core kernel (KLSH_PROJECT=mfma): bit-exact, but at d <= 64 its
   // per-pair epilogue (bound test + ballots) costs about what the packed chains cost — measured
   // 161-167 vs 140-145 us per C2 launch — so the packed VALU kernel stays the default

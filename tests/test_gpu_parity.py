@@ -98,7 +98,7 @@ def test_hash_keys_close_calls_vs_oracle(engine, oracle):
     from kmerlsh_amd import _native
 
     rng = np.random.default_rng(11)
-    for d, h in [(64, 23), (32, 18), (16, 9)]:
+    for d, h in [(64, 23), (32, 18), (16, 9), (512, 20), (100, 31), (72, 5)]:
         w, _ = _native.hyperplanes(7 + d, 0, h, d)
         w64 = w.astype(np.float64)
         rows = rng.normal(0, 1, size=(4000, d))
