@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <numeric>
@@ -144,6 +145,18 @@ struct klsh_ctx {
   size_t drec_cap = 0, drec_all_cap = 0;  // words
   uint64_t shard_cap = 0;
   double t_enqueued = 0.0;  // diagnostics (KLSH_ITER_LOG): host time when an iteration was queued
+  // Counters through mapped pinned memory (klsh::Publish): the host polls pub_seq instead of a
+  // copy launch + stream sync after every iteration.  KLSH_ZERO_COPY=0: the copy + sync.
+  Counters* pub_host = nullptr;   // host view
+  Counters* pub_dev = nullptr;    // device view of the same memory
+  uint32_t* pub_seq_host = nullptr;
+  uint32_t* pub_seq_dev = nullptr;
+  uint32_t pub_seq = 0;
+  bool ctr_clean = false;  // *ctr is known to be zero (the publisher zeroed it)
+  bool zero_copy = [] {
+    const char* e = getenv("KLSH_ZERO_COPY");
+    return !(e && e[0] == '0');
+  }();
   // KLSH_GRID_HINTS=1: size the big-run grids from the previous iteration's run counts.  Off by
   // default: measured slower on C2 (346 -> 370 ms; with fewer pending big-run workgroups the
   // small-run waves take the CUs the big runs need).
@@ -247,6 +260,9 @@ struct klsh_ctx {
     dfree(ctr);
     if (h_ctr) (void)hipHostFree(h_ctr);
     h_ctr = nullptr;
+    if (pub_host) (void)hipHostFree(pub_host);
+    pub_host = nullptr;
+    pub_dev = nullptr;
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e), e = nullptr;
     for (int i = 0; i < klsh::kMergeStreams; ++i) {
@@ -351,8 +367,32 @@ struct klsh_ctx {
   const float* hyperplane_ptr(uint64_t k) const { return W + (k - w_k0) * (uint64_t)dp; }
 
   int sync_counters() {
+    ctr_clean = false;
     KLSH_HIP(hipMemcpyAsync(h_ctr, ctr, sizeof(Counters), hipMemcpyDeviceToHost, stream));
     KLSH_HIP(hipStreamSynchronize(stream));
+    return check_device_err();
+  }
+  // Wait for the counters the compaction published with sequence number `seq` (spin on the
+  // mapped word; every few thousand polls the stream is queried, so a failed kernel is reported
+  // instead of waited for).
+  int wait_published(uint32_t seq) {
+    volatile uint32_t* p = pub_seq_host;
+    uint64_t spins = 0;
+    while (*p != seq) {
+      __builtin_ia32_pause();
+      if ((++spins & 0xFFFu) == 0) {
+        const hipError_t q = hipStreamQuery(stream);
+        if (q == hipSuccess) {
+          std::atomic_thread_fence(std::memory_order_seq_cst);
+          if (*p != seq) return fail(KLSH_E_HIP, "counters not published by a finished stream");
+          break;
+        }
+        if (q != hipErrorNotReady) return fail(KLSH_E_HIP, std::string("stream: ") + hipGetErrorString(q));
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    memcpy(h_ctr, (const void*)pub_host, sizeof(Counters));
+    ctr_clean = true;
     return check_device_err();
   }
   int check_device_err() const {
@@ -425,6 +465,22 @@ klsh_ctx* klsh_create(int device, int* err) {
   ok = ok && hipMalloc((void**)&c->ctr, sizeof(Counters)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) == hipSuccess;
   ok = ok && hipMemset(c->ctr, 0, sizeof(Counters)) == hipSuccess;  // err starts clear
+  if (ok && c->zero_copy) {
+    void* hp = nullptr;
+    void* dp = nullptr;
+    const size_t bytes = sizeof(Counters) + 64;
+    if (hipHostMalloc(&hp, bytes, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+        hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
+      memset(hp, 0, bytes);
+      c->pub_host = static_cast<Counters*>(hp);
+      c->pub_dev = static_cast<Counters*>(dp);
+      c->pub_seq_host = reinterpret_cast<uint32_t*>(static_cast<char*>(hp) + sizeof(Counters));
+      c->pub_seq_dev = reinterpret_cast<uint32_t*>(static_cast<char*>(dp) + sizeof(Counters));
+    } else {
+      if (hp) (void)hipHostFree(hp);
+      c->zero_copy = false;  // fall back to copy + sync
+    }
+  }
   if (!ok) {
     delete c;
     fail(KLSH_E_HIP, "stream/event/counter allocation failed");
@@ -610,12 +666,20 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->mw, ctx->ctr, s);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[3], s));
-  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
+  const bool zc = sync && ctx->zero_copy;
+  klsh::Publish pub{ctx->pub_dev, ctx->pub_seq_dev, ++ctx->pub_seq};
+  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s, zc ? &pub : nullptr);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
   if (!sync) return 0;  // the caller fetches the counters with its own exchange
   ctx->t_enqueued = now_ms();
-  if (int e = ctx->sync_counters()) return e;
+  if (zc) {
+    if (int e = ctx->wait_published(pub.seq)) return e;
+  } else {
+    ctx->ctr_clean = false;
+    if (int e = ctx->sync_counters()) return e;
+  }
+  if (timed && zc) KLSH_HIP(hipEventSynchronize(ctx->ev[4]));
   if (timed && st) {
     st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
     st->compact_ms += elapsed(ctx->ev[3], ctx->ev[4]);
@@ -742,7 +806,8 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     st->hyperplanes += (uint64_t)h;
     if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h, &st->host_ms)) return e;
 
-    KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    if (!ctx->ctr_clean) KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    ctx->ctr_clean = false;
     KLSH_HIP(hipEventRecord(ctx->ev[0], s));
     klsh::launch_project(ctx->rows, ctx->order, ctx->keys, (uint32_t)n, ctx->hyperplane_ptr(k), h,
                          0u, s, &ctx->pw);
@@ -891,7 +956,8 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
     if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h, &st->host_ms)) return e;
 
     // 1. keys of my rows, key-range ownership, send counts
-    KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    if (!ctx->ctr_clean) KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    ctx->ctr_clean = false;
     KLSH_HIP(hipEventRecord(ctx->ev[0], s));
     klsh::launch_project(ctx->rows, ctx->order, ctx->keys, n_g, ctx->hyperplane_ptr(k), h, 0u, s,
                          &ctx->pw);
@@ -1079,6 +1145,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   float threshold = max_similarity;
 
   memset(ctx->mw.hint, 0, sizeof(ctx->mw.hint));  // no run counts seen yet in this call
+  ctx->ctr_clean = false;
   ctx->mw.hint_small = 0;
   // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
   // lshash.cc:36-42), so repeated timed calls never reuse a previous call's tables.

@@ -144,9 +144,18 @@ void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
                   float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s);
 
+// Counters handed to the host through mapped pinned memory (no copy launch, no stream sync): the
+// compaction's last workgroup writes *ctr (total filled in) to `host`, zeroes *ctr for the next
+// iteration, then writes `seq` to *seq_host (system-scope release); the host polls *seq_host.
+struct Publish {
+  Counters* host;     // device pointer of the mapped host copy (nullptr: no publishing)
+  uint32_t* seq_host;
+  uint32_t seq;
+};
+
 // out[0..total) = slots[p] for p with slots[p] != kInvalid, stable; ctr->total = count.
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
-                    Counters* ctr, hipStream_t s);
+                    Counters* ctr, hipStream_t s, const Publish* pub = nullptr);
 
 // Mode-C producer: rows x[i] (slot i) from counts (d x bs, sample-major), LUT ln(c+1),
 // v_kmers; order[] = kept rows (sum > 0.1 d) compacted; ctr->total = kept count.

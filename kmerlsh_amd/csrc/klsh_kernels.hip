@@ -748,11 +748,28 @@ __global__ __launch_bounds__(256) void k_compact_count(const uint32_t* __restric
   if (t == 0) counts[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
+// Publish the iteration's counters to the host (see Publish), `total` filled in.
+__device__ __forceinline__ void publish_counters(Counters* ctr, uint32_t total, const Publish& pub) {
+  Counters c = *ctr;
+  c.total = total;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&c);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(pub.host);
+  for (int i = 0; i < (int)(sizeof(Counters) / 4); ++i) {
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    reinterpret_cast<uint32_t*>(ctr)[i] = 0u;  // the next iteration starts from zero
+  }
+  __threadfence_system();
+  __hip_atomic_store(pub.seq_host, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_publish(Counters* ctr, Publish pub) { publish_counters(ctr, ctr->total, pub); }
+
 __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restrict__ slots,
                                                        uint32_t n,
                                                        const uint32_t* __restrict__ counts,
                                                        uint32_t* __restrict__ out,
-                                                       uint32_t* __restrict__ total) {
+                                                       uint32_t* __restrict__ total,
+                                                       Counters* ctr, Publish pub) {
   constexpr int K = kCompactTile / 256;
   __shared__ uint32_t cnt[K * 4], pre[K * 4 + 1], wsum[4];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -786,19 +803,24 @@ __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restric
 #pragma unroll
   for (int k = 0; k < K; ++k)
     if (v[k] != kInvalid) out[pre[k * 4 + wv] + (uint32_t)__popcll(m[k] & below)] = v[k];
-  if (blockIdx.x == gridDim.x - 1 && t == 0) *total = pre[K * 4];
+  if (blockIdx.x == gridDim.x - 1 && t == 0) {
+    *total = pre[K * 4];
+    if (pub.host) publish_counters(ctr, pre[K * 4], pub);
+  }
 }
 
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
-                    Counters* ctr, hipStream_t s) {
+                    Counters* ctr, hipStream_t s, const Publish* pub) {
   if (scan_variant() == 2 || n == 0) {  // KLSH_SCAN=3k: the generic scan (A/B)
     device_scan(SrcLive{slots}, DstCompact{slots, out}, n, tile_sums, &ctr->total, &ctr->err, s);
+    if (pub) k_publish<<<1, 1, 0, s>>>(ctr, *pub);  // after the scan: total is final
     return;
   }
   const uint32_t ntiles = (n + kCompactTile - 1) / kCompactTile;
   uint32_t* counts = tile_sums + kScanSumsWord;
   k_compact_count<<<ntiles, 256, 0, s>>>(slots, n, counts);
-  k_compact_apply<<<ntiles, 256, 0, s>>>(slots, n, counts, out, &ctr->total);
+  k_compact_apply<<<ntiles, 256, 0, s>>>(slots, n, counts, out, &ctr->total, ctr,
+                                         pub ? *pub : Publish{nullptr, nullptr, 0u});
 }
 
 // ========================================================================== radix sort ==========
