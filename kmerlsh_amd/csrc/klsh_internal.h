@@ -18,7 +18,8 @@ constexpr uint32_t kSortStatusWord = 2048;  // sort workspace: small words, then
 // workspace words (64 small words + one u64 status word per scan tile; at least what the
 // three-kernel scan variant needs).  Both are zeroed once at allocation.
 inline uint64_t sort_ws_words(uint64_t slots) {
-  return kSortStatusWord + 512ull * ((slots + kRadixTile - 1) / kRadixTile) + 256;
+  // onesweep status (256 u64 per tile) or an LSD [digit][tile] histogram of up to 1024 digits
+  return kSortStatusWord + 1024ull * ((slots + kRadixTile - 1) / kRadixTile) + 256;
 }
 // Scan workspace (u32 words): [0, 64) ticket / done / epoch of the look-back scan, then its 64-bit
 // tile status words (room for 2^32 items), then the tile sums of the multi-kernel scans and of

@@ -957,6 +957,107 @@ __global__ __launch_bounds__(256) void k_radix_scatter_lds(const uint32_t* __res
   }
 }
 
+// ------------------------------------------------------------- wider digits (small sorts) -----
+// The same two kernels for a B-bit digit (B = 9 or 10), so a key of up to 2B bits sorts in two
+// passes instead of three: the small late iterations (h <= 20) pay per launch, not per byte.
+template <int B>
+__global__ __launch_bounds__(256) void k_radix_hist_w(const uint32_t* __restrict__ keys, uint32_t n,
+                                                      int shift, uint32_t ntiles,
+                                                      uint32_t* __restrict__ hist) {
+  constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u;
+  __shared__ uint32_t c[RAD];
+  for (uint32_t d = threadIdx.x; d < RAD; d += 256) c[d] = 0;
+  __syncthreads();
+  const uint32_t base = blockIdx.x * (uint32_t)kRadixTile;
+  for (int r = 0; r < kRadixTile / 256; ++r) {
+    const uint32_t i = base + r * 256u + threadIdx.x;
+    if (i < n) atomicAdd(&c[(keys[i] >> shift) & MASK], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < RAD; d += 256) hist[d * ntiles + blockIdx.x] = c[d];
+}
+
+template <int B>
+__global__ __launch_bounds__(256) void k_radix_scatter_w(const uint32_t* __restrict__ kin,
+                                                         const uint32_t* __restrict__ vin,
+                                                         uint32_t* __restrict__ kout,
+                                                         uint32_t* __restrict__ vout, uint32_t n,
+                                                         int shift, uint32_t ntiles,
+                                                         const uint32_t* __restrict__ hist) {
+  constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u;
+  __shared__ uint32_t lk[kRadixTile], lv[kRadixTile];
+  __shared__ uint32_t gbase[RAD], lstart[RAD], run[RAD];
+  __shared__ uint32_t wcnt[4][RAD];
+  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+  const uint32_t tile0 = blockIdx.x * (uint32_t)kRadixTile;
+  const uint32_t m = min((uint32_t)kRadixTile, n - tile0);
+  for (uint32_t d = t; d < RAD; d += 256) {
+    gbase[d] = hist[d * ntiles + blockIdx.x];
+    run[d] = 0;
+    wcnt[0][d] = wcnt[1][d] = wcnt[2][d] = wcnt[3][d] = 0;
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < m; i += 256) atomicAdd(&wcnt[0][(kin[tile0 + i] >> shift) & MASK], 1u);
+  __syncthreads();
+  {  // tile-local digit offsets: exclusive scan of RAD counts, RAD / 256 per thread
+    constexpr uint32_t PER = RAD / 256;
+    uint32_t v[PER], acc = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      v[q] = wcnt[0][t * PER + q];
+      acc += v[q];
+    }
+    uint32_t total;
+    uint32_t pre = block_excl_scan_256(acc, &total);
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      lstart[t * PER + q] = pre;
+      pre += v[q];
+    }
+  }
+  for (uint32_t d = t; d < RAD; d += 256) wcnt[0][d] = 0;
+  __syncthreads();
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int r = 0; r < kRadixTile / 256; ++r) {
+    const uint32_t i = r * 256u + t;
+    const bool valid = i < m;
+    const uint32_t k = valid ? kin[tile0 + i] : 0u;
+    const uint32_t v = valid ? vin[tile0 + i] : 0u;
+    const uint32_t dig = (k >> shift) & MASK;
+    uint64_t match = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const bool bit = (dig >> b) & 1u;
+      const uint64_t mb = __ballot(bit);
+      match &= bit ? mb : ~mb;
+    }
+    const uint32_t rank = __popcll(match & lt_mask);
+    if (valid && rank == 0) wcnt[w][dig] = __popcll(match);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = lstart[dig] + run[dig] + rank;
+      for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dig];
+      lk[pos] = k;
+      lv[pos] = v;
+    }
+    __syncthreads();
+    if (valid && rank == 0) {  // the digits present this round: one updater each (lowest wave)
+      bool first = true;
+      for (uint32_t q = 0; q < w; ++q) first = first && wcnt[q][dig] == 0u;
+      if (first) run[dig] += wcnt[0][dig] + wcnt[1][dig] + wcnt[2][dig] + wcnt[3][dig];
+    }
+    __syncthreads();
+    if (valid && rank == 0) wcnt[w][dig] = 0;
+    __syncthreads();
+  }
+  for (uint32_t e = t; e < m; e += 256) {
+    const uint32_t k = lk[e];
+    const uint32_t d = (k >> shift) & MASK;
+    kout[gbase[d] + (e - lstart[d])] = k;
+    vout[gbase[d] + (e - lstart[d])] = lv[e];
+  }
+}
+
 // ---------------------------------------------------------------- onesweep (single pass) ------
 // The same stable LSD sort with one kernel per digit pass: an up-front histogram of every pass's
 // digits (one read of the keys) gives each digit's global base; the scatter kernels take tiles in
@@ -1158,6 +1259,28 @@ void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t
   }
   // LSD passes: [digit][tile] histogram in the status area (the onesweep words stay intact)
   uint32_t* h = hist + kSortStatusWord;
+  // Two passes of 9- or 10-bit digits instead of three of 8 when the key has 17..20 bits and the
+  // wider histogram stays small (KLSH_SORT_WIDE=0: always 8-bit digits)
+  static const bool wide_ok = [] {
+    const char* e = getenv("KLSH_SORT_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  if (wide_ok && n > 1 && bits >= 17 && bits <= 20 && (uint64_t)ntiles * 1024u <= (1u << 20)) {
+    const int B = (bits + 1) / 2;
+    for (int shift = 0; shift < bits; shift += B) {
+      const uint32_t rad = 1u << B;
+      if (B == 9) k_radix_hist_w<9><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, h);
+      else k_radix_hist_w<10><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, h);
+      device_scan(SrcArray{h}, DstExclusive{h}, rad * ntiles, tile_sums, &ctr->total, &ctr->err, s);
+      if (B == 9) k_radix_scatter_w<9><<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, h);
+      else k_radix_scatter_w<10><<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, h);
+      std::swap(ki, ko);
+      std::swap(vi, vo);
+    }
+    *out_k = ki;
+    *out_v = vi;
+    return;
+  }
   static const bool scatter_lds = [] {  // KLSH_SCATTER=direct: the unstaged scatter
     const char* e = getenv("KLSH_SCATTER");
     return !(e && std::string(e) == "direct");

@@ -1774,7 +1774,14 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
     launch_big<D, 384, 256, false>(w, 1, slots, dc, r, ctr, n, f.lane(0));
   launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
-  launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
+  static const bool big128_wide = [] {  // KLSH_BIG128_NT=256: 4 waves per 65..128-row run (A/B)
+    const char* e = getenv("KLSH_BIG128_NT");
+    return e && atoi(e) == 256;
+  }();
+  if (big128_wide)
+    launch_big<D, 128, 256, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
+  else
+    launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   if (small_fused()) {
     // a persistent grid: 2x the batches of the previous iteration (the kernel strides over its
     // batches, so any grid is correct), at most what the GPU holds twice over

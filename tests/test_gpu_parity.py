@@ -58,6 +58,7 @@ def test_hash_keys_match_reference(engine, name):
     (1, 8, 1), (2, 1, 2), (2047, 8, 300), (2048, 13, 1 << 13), (2049, 16, 5),
     (100_000, 17, 1 << 17), (300_000, 23, 1000), (1_000_003, 22, 1 << 22), (5_000_000, 23, 1 << 23),
     (200_000, 31, 1 << 31), (70_000, 0, 1),
+    (390_000, 18, 1 << 18), (1_500_000, 20, 1 << 20), (300_000, 19, 700), (150_000, 17, 1 << 17),
 ])
 def test_bucket_sort_is_stable_counting_sort(engine, n, bits, spread):
     """merge_hashtable (cluster.cc:15-30) scatters rows into lsh_table[key] in row order: the
