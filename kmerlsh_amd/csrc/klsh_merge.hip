@@ -55,6 +55,8 @@ __device__ unsigned long long g_mprof[8][8];
 #define MPROF_T() wall_clock64()
 #define MPROF_ADD(c, k, v) atomicAdd(&g_mprof[c][k], (unsigned long long)(v))
 #define MPROF_MAX(c, k, v) atomicMax(&g_mprof[c][k], (unsigned long long)(v))
+__device__ unsigned long long g_sprof[8][8];  // small-run batches per G class: batches, clocks in
+                                              // stage, pairwise, walk, write-back
 __device__ unsigned long long g_wprof[8][8];  // walk phases in shader clocks: find, select+
                                               // consensus, dots, bits, steps, find rounds
 #define WPROF_CLK() __builtin_amdgcn_s_memtime()
@@ -203,6 +205,10 @@ __device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucke
 #define KLSH_ROW_PREFETCH 0
 #endif
 constexpr bool kRowPrefetch = KLSH_ROW_PREFETCH != 0;
+#ifndef KLSH_LAZY_META
+#define KLSH_LAZY_META 1
+#endif
+constexpr bool kLazyMeta = KLSH_LAZY_META != 0;  // -DKLSH_LAZY_META=0: eager loads (A/B build)
 
 template <int G, int D, class Prefetch>
 __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
@@ -216,12 +222,20 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
   const uint32_t gbase = lane - g;
   const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << (G & 63)) - 1ull) << gbase);
   float* myrow = lds + lane * ST;
+  [[maybe_unused]] const uint64_t sp0 = WPROF_CLK();
+  [[maybe_unused]] uint64_t sp1 = 0, sp2 = 0, sp3 = 0;
   {
     const bool valid = g < b;
     float nrm = valid ? r.nrm[slot] : 0.0f;
-    uint32_t cnt = valid ? r.cnt[slot] : 0u;
-    uint32_t hd = valid ? r.head[slot] : 0u;
-    const uint32_t tl = valid ? r.tail[slot] : 0u;
+    // member count / list ends: only a merge needs them, and most batches have none — they are
+    // loaded after the pairwise decisions, by waves that found a matching pair (saves three
+    // random 4-B reads per row, as much traffic as the row itself)
+    uint32_t cnt = 0u, hd = 0u, tl = 0u;
+    if (!kLazyMeta && valid) {
+      cnt = r.cnt[slot];
+      hd = r.head[slot];
+      tl = r.tail[slot];
+    }
     if constexpr (kRowPrefetch) {
       store_rows<D>(rb, lds);  // rows gathered one batch ahead -> LDS row l = lane l's row
     } else {
@@ -233,6 +247,10 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
     float x[D];
     load_row<D>(myrow, x);
     const uint32_t bmax = wave_max(b);
+#ifdef KLSH_MERGE_PROF
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    sp1 = WPROF_CLK();
+#endif
 
     // 1. every pairwise decision of the run, each unordered pair once: lane g pairs with the
     //    rows k = 1 .. b/2 positions after it, cyclically.  decide(a, c) == decide(c, a) (same
@@ -265,6 +283,16 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
       share(k + 1, h1);
     }
 
+    if (kLazyMeta && __ballot(valid && full != 0ull)) {  // some run of the wave merges
+      if (valid) {
+        cnt = r.cnt[slot];
+        hd = r.head[slot];
+        tl = r.tail[slot];
+      }
+    }
+#ifdef KLSH_MERGE_PROF
+    sp2 = WPROF_CLK();
+#endif
     // 2. replay the walk on the bits.  Positions that find no candidate below them change
     //    nothing, so each round jumps straight to the first position q >= i whose row matches
     //    some row at a position below q (exclusive prefix-OR of row bits over positions).
@@ -326,9 +354,12 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
       }
     }
 
+#ifdef KLSH_MERGE_PROF
+    sp3 = WPROF_CLK();
+#endif
     // 3. write back: survivors in position order, kInvalid after; changed rows and metadata
     const uint32_t pos_slot = shfl32(slot, gbase + rowid);
-    if (valid) slots[p + g] = g < size ? pos_slot : kInvalid;
+    if (valid && size < b) slots[p + g] = g < size ? pos_slot : kInvalid;  // runs that merged
     if (valid && alive && dirty) {
       float* xo = r.x + (size_t)slot * r.dp;
 #pragma unroll
@@ -342,6 +373,18 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
     if (valid && !alive) r.cnt[slot] = 0u;
     wave_lds_fence();
   }
+#ifdef KLSH_MERGE_PROF
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (lane == 0) {
+    constexpr int c = G == 4 ? 1 : G == 8 ? 2 : G == 16 ? 3 : G == 32 ? 4 : 5;
+    const uint64_t sp4 = WPROF_CLK();
+    atomicAdd(&g_sprof[c][0], 1ull);
+    atomicAdd(&g_sprof[c][1], sp1 - sp0);
+    atomicAdd(&g_sprof[c][2], sp2 - sp1);
+    atomicAdd(&g_sprof[c][3], sp3 - sp2);
+    atomicAdd(&g_sprof[c][4], sp4 - sp3);
+  }
+#endif
 }
 
 // One lane per run: runs of 2..64 rows go to their size-class list, longer ones to the big /
@@ -1880,9 +1923,17 @@ void merge_prof_dump(FILE* f) {
                 names[c], wpf[c][4], (double)wpf[c][0] / wpf[c][4], (double)wpf[c][1] / wpf[c][4],
                 (double)wpf[c][2] / wpf[c][4], (double)wpf[c][3] / wpf[c][4],
                 (double)wpf[c][5] / wpf[c][4]);
+  unsigned long long spf[8][8];
+  if (hipMemcpyFromSymbol(spf, HIP_SYMBOL(g_sprof), sizeof(spf)) == hipSuccess)
+    for (int c = 1; c < 6; ++c)
+      if (spf[c][0])
+        fprintf(f, "[sprof] G=%-2d batches %9llu  clocks/batch: stage %7.0f  pairwise %7.0f  walk %7.0f"
+                   "  write %7.0f\n", 2 << c, spf[c][0], (double)spf[c][1] / spf[c][0],
+                (double)spf[c][2] / spf[c][0], (double)spf[c][3] / spf[c][0], (double)spf[c][4] / spf[c][0]);
   unsigned long long z[8][8] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mprof), z, sizeof(z));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), z, sizeof(z));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sprof), z, sizeof(z));
 #else
   (void)f;
 #endif
