@@ -217,7 +217,7 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
                                             uint32_t* slots, const Decider& dc, const Rows& r,
                                             float* lds, uint32_t* dlist, Counters* ctr) {
   constexpr int ST = D + 4;  // padded row stride: 16 lanes of a ds_read_b128 hit distinct banks
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = __lane_id();
   const uint32_t g = lane & (G - 1);
   const uint32_t gbase = lane - g;
   const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << (G & 63)) - 1ull) << gbase);
@@ -485,10 +485,12 @@ __device__ __forceinline__ void pair_batch(const uint2* __restrict__ list, uint3
   if (dlist) append_slot(merged, s0, dlist, &ctr->n_delta);
 }
 
+// One wave's share of the small-run batches: waves `wave`, `wave + nwaves`, ... of the batch
+// space; lds = this wave's 64 * (D + 4) floats.
 template <int D>
-__global__ __launch_bounds__(64) void k_merge_small(MergeWork w, uint32_t* __restrict__ slots,
-                                                    Decider dc, Rows r, Counters* ctr) {
-  __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
+__device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restrict__ slots,
+                                           const Decider& dc, const Rows& r, Counters* ctr,
+                                           float* lds, uint32_t wave, uint32_t nwaves) {
   constexpr int NC = kGroupClasses;
   uint32_t n[NC], nb[NC], start[NC + 1];
 #pragma unroll
@@ -512,7 +514,7 @@ __global__ __launch_bounds__(64) void k_merge_small(MergeWork w, uint32_t* __res
     start[NC] = a;  // total
   }
   const uint32_t total = start[NC];
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = __lane_id();
   auto locate = [&](uint32_t t, int& c, uint32_t& bi) {
     c = 0;
 #pragma unroll
@@ -539,11 +541,11 @@ __global__ __launch_bounds__(64) void k_merge_small(MergeWork w, uint32_t* __res
   float4 rb[1];
   uint2 e;
   uint32_t slot;
-  fetch(blockIdx.x, e, slot);
-  for (uint32_t t = blockIdx.x; t < total; t += gridDim.x) {
+  fetch(wave, e, slot);
+  for (uint32_t t = wave; t < total; t += nwaves) {
     uint2 e_next;
     uint32_t slot_next;
-    fetch(t + gridDim.x, e_next, slot_next);
+    fetch(t + nwaves, e_next, slot_next);
     int c;
     uint32_t bi;
     locate(t, c, bi);
@@ -567,6 +569,13 @@ static bool big384_rows_lds() {  // KLSH_BIG384_LDS=0: 129..384-row runs read ro
     return !(e && e[0] == '0');
   }();
   return v;
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void k_merge_small(MergeWork w, uint32_t* __restrict__ slots,
+                                                    Decider dc, Rows r, Counters* ctr) {
+  __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
+  small_loop<D>(w, slots, dc, r, ctr, lds, blockIdx.x, gridDim.x);
 }
 
 static bool small_fused() {  // KLSH_SMALL=split: one kernel per size class on the streams (A/B)
@@ -1120,13 +1129,16 @@ struct BigLayout {
   static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 7;
 };
 
+// The runs li = first, first + stride, ... (< count) of list `list` (size class cls), one
+// workgroup of NT lanes per run, with smem = BigLayout<D, RB, ROWS_LDS>::bytes of LDS.
 template <int D, int RB, int NT, bool ROWS_LDS>
-__global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list, int cls,
-                                                  uint32_t* __restrict__ slots, Decider dc,
-                                                  Rows r, Counters* ctr, uint32_t* dlist) {
+__device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls, uint32_t count,
+                                         uint32_t first, uint32_t stride,
+                                         uint32_t* __restrict__ slots, const Decider& dc,
+                                         const Rows& r, Counters* ctr, uint32_t* dlist,
+                                         unsigned char* smem) {
   using L = BigLayout<D, RB, ROWS_LDS>;
   constexpr int ST = L::ST, W = L::W, NW = NT / 64;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* rows = reinterpret_cast<float*>(smem + L::rows);  // rows, or one staged column block
   uint64_t* P = reinterpret_cast<uint64_t*>(smem + L::P);  // [row][W] position-space masks
   uint32_t* slot = reinterpret_cast<uint32_t*>(smem + L::meta);
@@ -1138,13 +1150,11 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
   float* sq = reinterpret_cast<float*>(slot + 6 * RB);  // sqrtf(nrm), distance.cc:37
   __shared__ uint32_t wbuf[2 * NW];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t count =
-      __hip_atomic_load(&ctr->n_big[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   auto row_ptr = [&](uint32_t a) -> const float* {
     return ROWS_LDS ? rows + a * ST : r.x + (size_t)slot[a] * r.dp;
   };
 
-  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+  for (uint32_t li = first; li < count; li += stride) {
     const uint2 e = list[li];
     const uint32_t p = e.x, b = e.y;
     const uint32_t nblk = (b + 63) / 64;
@@ -1260,6 +1270,50 @@ __global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list
       MPROF_MAX(cls, 6, b);
     }
 #endif
+  }
+}
+
+template <int D, int RB, int NT, bool ROWS_LDS>
+__global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list, int cls,
+                                                  uint32_t* __restrict__ slots, Decider dc,
+                                                  Rows r, Counters* ctr, uint32_t* dlist) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t count =
+      __hip_atomic_load(&ctr->n_big[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  big_runs<D, RB, NT, ROWS_LDS>(list, cls, count, blockIdx.x, gridDim.x, slots, dc, r, ctr, dlist,
+                                smem);
+}
+
+// Small iterations: every merge class in ONE launch on the main stream (no fork/join across
+// streams, ≈35 us per iteration there): workgroups [0, nbig) take the 65..896-row runs (the
+// longest class first), the others run four small-run waves each.
+template <int D>
+__global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __restrict__ slots,
+                                                    Decider dc, Rows r, Counters* ctr,
+                                                    uint32_t nbig) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (blockIdx.x < nbig) {
+    uint32_t cnt[kBigClasses];
+#pragma unroll
+    for (int c = 0; c < kBigClasses; ++c)
+      cnt[c] = __hip_atomic_load(&ctr->n_big[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // one index space, 385..896 first, then 129..384, then 65..128
+    const uint32_t a2 = cnt[2], a1 = a2 + cnt[1], total = a1 + cnt[0];
+    for (uint32_t li = blockIdx.x; li < total; li += nbig) {  // block-uniform
+      if (li < a2)
+        big_runs<D, 896, 256, false>(w.big[2], 2, li + 1, li, 1u << 30, slots, dc, r, ctr, w.dlist, smem);
+      else if (li < a1)
+        big_runs<D, 384, 256, true>(w.big[1], 1, li - a2 + 1, li - a2, 1u << 30, slots, dc, r, ctr,
+                                    w.dlist, smem);
+      else
+        big_runs<D, 128, 256, true>(w.big[0], 0, li - a1 + 1, li - a1, 1u << 30, slots, dc, r, ctr,
+                                    w.dlist, smem);
+      __syncthreads();
+    }
+  } else {
+    const uint32_t wv = threadIdx.x >> 6;
+    float* lds = reinterpret_cast<float*>(smem) + wv * 64 * (D + 4);
+    small_loop<D>(w, slots, dc, r, ctr, lds, (blockIdx.x - nbig) * 4u + wv, (gridDim.x - nbig) * 4u);
   }
 }
 
@@ -1808,6 +1862,25 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   auto grid = [&](int c, uint32_t per_wave) {
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
+  static const uint32_t tail_max = [] {  // KLSH_TAIL_MERGE: positions below which one launch
+    const char* e = getenv("KLSH_TAIL_MERGE");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 20);
+  }();
+  if (n < tail_max && small_fused()) {
+    using L896 = BigLayout<D, 896, false>;
+    using L384 = BigLayout<D, 384, true>;
+    using L128 = BigLayout<D, 128, true>;
+    constexpr size_t small_lds = 4 * 64 * (D + 4) * sizeof(float);
+    constexpr size_t lds = std::max({L896::bytes, L384::bytes, L128::bytes, small_lds});
+    static const bool lds_ok =
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_tail<D>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
+    (void)lds_ok;
+    launch_huge(w, slots, dc, r, ctr, n, s);
+    const uint32_t nbig = 64, nsmall = 256;
+    k_merge_tail<D><<<nbig + nsmall, 256, lds, s>>>(w, slots, dc, r, ctr, nbig);
+    return;
+  }
   const Fork f(w, s);
   // longest walks first on each stream; the longest runs (few, long walks) on the main stream,
   // concurrent with the auxiliary ones (it waits for them at the join)
