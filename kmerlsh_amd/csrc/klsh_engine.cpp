@@ -23,6 +23,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <functional>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -153,6 +154,17 @@ struct klsh_ctx {
   uint32_t* pub_seq_dev = nullptr;
   uint32_t pub_seq = 0;
   bool ctr_clean = false;  // *ctr is known to be zero (the publisher zeroed it)
+  // Queued-ahead projection (small iterations, where no bucket can be oversize): the next
+  // iteration's sign-hash is enqueued behind the compaction, reading N from n_next_dev, before
+  // the host has the counters.  KLSH_QUEUE_AHEAD=0: off.
+  uint32_t* n_next_dev = nullptr;
+  bool spec_pending = false;
+  uint64_t spec_k = 0;
+  int spec_ev = 0;
+  bool queue_ahead = [] {
+    const char* e = getenv("KLSH_QUEUE_AHEAD");
+    return !(e && e[0] == '0');
+  }();
   bool zero_copy = [] {
     const char* e = getenv("KLSH_ZERO_COPY");
     return !(e && e[0] == '0');
@@ -260,6 +272,7 @@ struct klsh_ctx {
     dfree(ctr);
     if (h_ctr) (void)hipHostFree(h_ctr);
     h_ctr = nullptr;
+    dfree(n_next_dev);
     if (pub_host) (void)hipHostFree(pub_host);
     pub_host = nullptr;
     pub_dev = nullptr;
@@ -465,6 +478,8 @@ klsh_ctx* klsh_create(int device, int* err) {
   ok = ok && hipMalloc((void**)&c->ctr, sizeof(Counters)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) == hipSuccess;
   ok = ok && hipMemset(c->ctr, 0, sizeof(Counters)) == hipSuccess;  // err starts clear
+  ok = ok && hipMalloc((void**)&c->n_next_dev, 64) == hipSuccess &&
+       hipMemset(c->n_next_dev, 0, 64) == hipSuccess;
   if (ok && c->zero_copy) {
     void* hp = nullptr;
     void* dp = nullptr;
@@ -660,17 +675,19 @@ int klsh_restore(klsh_ctx* ctx) {
 // Ends with the counters on the host: total (survivors), n_over (oversize runs), n_delta.
 static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
                       int bucket_thr, uint32_t* out, klsh_stats* st, bool timed,
-                      bool sync = true) {
+                      bool sync = true, const std::function<int(uint32_t*)>* after = nullptr) {
   hipStream_t s = ctx->stream;
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
   klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->mw, ctx->ctr, s);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[3], s));
   const bool zc = sync && ctx->zero_copy;
-  klsh::Publish pub{ctx->pub_dev, ctx->pub_seq_dev, ++ctx->pub_seq};
+  klsh::Publish pub{ctx->pub_dev, ctx->pub_seq_dev, ++ctx->pub_seq, ctx->n_next_dev};
   klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s, zc ? &pub : nullptr);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
+  if (zc && after)  // work queued behind the compaction before the host waits for it
+    if (int e = (*after)(out)) return e;
   if (!sync) return 0;  // the caller fetches the counters with its own exchange
   ctx->t_enqueued = now_ms();
   if (zc) {
@@ -744,9 +761,10 @@ static int merge_nested(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, f
 // ctx->n_live updated.
 static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
                              int bucket_thr, uint32_t seed_base, uint64_t* rng_counter,
-                             klsh_stats* st, bool timed) {
+                             klsh_stats* st, bool timed,
+                             const std::function<int(uint32_t*)>* after = nullptr) {
   uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
-  if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, st, timed)) return e;
+  if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, st, timed, true, after)) return e;
   // the next iteration's big-run grids: twice this iteration's run counts (plus slack)
   uint32_t next_hint[klsh::kBigClasses + 1];
   for (int c = 0; c < klsh::kBigClasses; ++c) next_hint[c] = 2 * ctx->h_ctr->n_big[c] + 4;
@@ -806,13 +824,20 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     st->hyperplanes += (uint64_t)h;
     if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h, &st->host_ms)) return e;
 
-    if (!ctx->ctr_clean) KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    // the projection: queued by the previous iteration (device-side N), or now
+    const bool queued = ctx->spec_pending;
+    ctx->spec_pending = false;
+    if (queued && ctx->spec_k != k) return fail(KLSH_E_STATE, "queued projection out of step");
+    const int e0 = queued ? ctx->spec_ev : 0;
+    if (!queued) {
+      if (!ctx->ctr_clean) KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+      KLSH_HIP(hipEventRecord(ctx->ev[e0], s));
+      klsh::launch_project(ctx->rows, ctx->order, ctx->keys, (uint32_t)n, ctx->hyperplane_ptr(k), h,
+                           0u, s, &ctx->pw);
+      KLSH_HIP(hipGetLastError());
+      KLSH_HIP(hipEventRecord(ctx->ev[e0 + 1], s));
+    }
     ctx->ctr_clean = false;
-    KLSH_HIP(hipEventRecord(ctx->ev[0], s));
-    klsh::launch_project(ctx->rows, ctx->order, ctx->keys, (uint32_t)n, ctx->hyperplane_ptr(k), h,
-                         0u, s, &ctx->pw);
-    KLSH_HIP(hipGetLastError());
-    KLSH_HIP(hipEventRecord(ctx->ev[1], s));
     uint32_t *fk = nullptr, *fv = nullptr;
     klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n, h, ctx->hist,
                      ctx->tile_sums, ctx->ctr, &fk, &fv, s);
@@ -845,10 +870,30 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
         fclose(f);
       }
     }
+    // Queue the next iteration's projection behind this compaction when no bucket of this
+    // iteration can be oversize (so no nestedCluster can change rows or draw hyperplanes first).
+    const bool ahead = ctx->queue_ahead && ctx->zero_copy && it + 1 < it_end &&
+                       bucket_size_threshold >= 0 && n <= (uint64_t)bucket_size_threshold &&
+                       klsh::project_device_n_ok(ctx->d) && !getenv("KLSH_BUCKET_STATS");
+    const std::function<int(uint32_t*)> queue_next = [&](uint32_t* next_order) -> int {
+      const uint64_t k_next = k + (uint64_t)h;  // h_next <= h: inside the drawn window
+      if (int e = ctx->ensure_hyperplanes(seed_base, k_next, (uint64_t)h, &st->host_ms)) return e;
+      const int ne = e0 == 0 ? 6 : 0;
+      KLSH_HIP(hipEventRecord(ctx->ev[ne], s));
+      klsh::launch_project_device_n(ctx->rows, next_order, ctx->keys, (uint32_t)n,
+                                    ctx->hyperplane_ptr(k_next), ctx->n_next_dev, s);
+      KLSH_HIP(hipGetLastError());
+      KLSH_HIP(hipEventRecord(ctx->ev[ne + 1], s));
+      ctx->spec_pending = true;
+      ctx->spec_k = k_next;
+      ctx->spec_ev = ne;
+      return 0;
+    };
     if (int e = merge_and_compact(ctx, fk, fv, (uint32_t)n, threshold, bucket_size_threshold,
-                                  seed_base, rng_counter, st, ctx->phase_timing))
+                                  seed_base, rng_counter, st, ctx->phase_timing,
+                                  ahead ? &queue_next : nullptr))
       return e;
-    st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
+    st->project_ms += elapsed(ctx->ev[e0], ctx->ev[e0 + 1]);
     if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
     st->project_launches += 1;
     st->sum_rows += n;
@@ -1146,6 +1191,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
 
   memset(ctx->mw.hint, 0, sizeof(ctx->mw.hint));  // no run counts seen yet in this call
   ctx->ctr_clean = false;
+  ctx->spec_pending = false;
   ctx->mw.hint_small = 0;
   // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
   // lshash.cc:36-42), so repeated timed calls never reuse a previous call's tables.

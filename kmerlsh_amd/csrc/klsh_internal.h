@@ -128,6 +128,13 @@ struct ProjectWork {
 
 // ---- launch wrappers (all asynchronous on `s`) ------------------------------------------------
 // keys[p] = sign-hash of row slots[p] against h hyperplanes W (h x dp), OR'ed with key_or.
+// The packed projection of an iteration queued before its row count is known: n and h come from
+// the device word n_dev (written by the previous compaction), n_max bounds the grid.  Only for
+// d in {8, 16, 32, 64} (project_device_n_ok).
+bool project_device_n_ok(int d);
+void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n_max,
+                             const float* W, const uint32_t* n_dev, hipStream_t s);
+
 // pw (may be null): the workspace that enables the matrix-core kernel for wide rows (d > 64).
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
                     const float* W, int h, uint32_t key_or, hipStream_t s,
@@ -152,6 +159,7 @@ struct Publish {
   Counters* host;     // device pointer of the mapped host copy (nullptr: no publishing)
   uint32_t* seq_host;
   uint32_t seq;
+  uint32_t* n_next;   // device word that also receives the survivor count (may be null)
 };
 
 // out[0..total) = slots[p] for p with slots[p] != kInvalid, stable; ctr->total = count.

@@ -104,14 +104,22 @@ __device__ __forceinline__ void pk_mac_hi(f32x2& acc, f32x2 w, f32x2 x) {
 // RPL rows per lane (rows p and p + 256 of the workgroup's 256 * RPL): every hyperplane read
 // from LDS feeds RPL rows — the single-row kernel is bound by the LDS broadcast reads about as
 // much as by the VALU.
+// n_dev (may be null): the row count lives on the device (an iteration queued before the
+// previous one's survivors were counted); then h = floor(log2 n) (cluster.cc:194) is derived here.
 template <int D, int CH, int RPL>
 __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X, int dp,
                                                     const uint32_t* __restrict__ slots,
                                                     uint32_t* __restrict__ keys, uint32_t n,
                                                     const float* __restrict__ W, int h,
-                                                    uint32_t key_or) {
+                                                    uint32_t key_or,
+                                                    const uint32_t* __restrict__ n_dev = nullptr) {
   constexpr int QMAX = kMaxHyperplanes / 4;
   __shared__ __attribute__((aligned(16))) float4 sw[QMAX * D];
+  if (n_dev) {
+    n = *n_dev;
+    if (n == 0) return;
+    h = 31 - __builtin_clz(n);
+  }
   const int nq = (h + 3) >> 2;
   for (int i = threadIdx.x; i < nq * D; i += 256) {
     const int q = i / D, k = i % D;
@@ -630,6 +638,22 @@ __global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X
   }
 }
 
+bool project_device_n_ok(int d) {
+  return d == 8 || d == 16 || d == 32 || d == 64;  // and the default variant (below)
+}
+
+void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n_max,
+                             const float* W, const uint32_t* n_dev, hipStream_t s) {
+  if (n_max == 0) return;
+  const dim3 grid((n_max + 255) / 256), block(256);
+  switch (r.d) {
+    case 8: k_project_pk<8, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev); break;
+    case 16: k_project_pk<16, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev); break;
+    case 32: k_project_pk<32, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev); break;
+    default: k_project_pk<64, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev); break;
+  }
+}
+
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
                     const float* W, int h, uint32_t key_or, hipStream_t s, const ProjectWork* pw) {
   if (n == 0) return;
@@ -752,6 +776,7 @@ __global__ __launch_bounds__(256) void k_compact_count(const uint32_t* __restric
 __device__ __forceinline__ void publish_counters(Counters* ctr, uint32_t total, const Publish& pub) {
   Counters c = *ctr;
   c.total = total;
+  if (pub.n_next) *pub.n_next = total;  // for an iteration already queued (device-side n)
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&c);
   uint32_t* dst = reinterpret_cast<uint32_t*>(pub.host);
   for (int i = 0; i < (int)(sizeof(Counters) / 4); ++i) {
@@ -820,7 +845,7 @@ void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* 
   uint32_t* counts = tile_sums + kScanSumsWord;
   k_compact_count<<<ntiles, 256, 0, s>>>(slots, n, counts);
   k_compact_apply<<<ntiles, 256, 0, s>>>(slots, n, counts, out, &ctr->total, ctr,
-                                         pub ? *pub : Publish{nullptr, nullptr, 0u});
+                                         pub ? *pub : Publish{nullptr, nullptr, 0u, nullptr});
 }
 
 // ========================================================================== radix sort ==========
