@@ -870,11 +870,14 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
         fclose(f);
       }
     }
-    // Queue the next iteration's projection behind this compaction when no bucket of this
-    // iteration can be oversize (so no nestedCluster can change rows or draw hyperplanes first).
+    // Queue the next iteration's projection behind this compaction.  If this iteration turns out
+    // to have oversize buckets (nestedCluster changes rows and draws hyperplanes first), the
+    // queued keys are simply recomputed; they go to ctx->keys, which the nested work must not be
+    // reading — so only when the sorted keys of this iteration are in the other buffer.
     const bool ahead = ctx->queue_ahead && ctx->zero_copy && it + 1 < it_end &&
-                       bucket_size_threshold >= 0 && n <= (uint64_t)bucket_size_threshold &&
-                       klsh::project_device_n_ok(ctx->d) && !getenv("KLSH_BUCKET_STATS");
+                       klsh::project_device_n_ok(ctx->d) && !getenv("KLSH_BUCKET_STATS") &&
+                       (fk != ctx->keys || (bucket_size_threshold >= 0 &&
+                                            n <= (uint64_t)bucket_size_threshold));
     const std::function<int(uint32_t*)> queue_next = [&](uint32_t* next_order) -> int {
       const uint64_t k_next = k + (uint64_t)h;  // h_next <= h: inside the drawn window
       if (int e = ctx->ensure_hyperplanes(seed_base, k_next, (uint64_t)h, &st->host_ms)) return e;
@@ -893,6 +896,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
                                   seed_base, rng_counter, st, ctx->phase_timing,
                                   ahead ? &queue_next : nullptr))
       return e;
+    if (ctx->spec_pending && *rng_counter != ctx->spec_k) ctx->spec_pending = false;  // nested ran
     st->project_ms += elapsed(ctx->ev[e0], ctx->ev[e0 + 1]);
     if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
     st->project_launches += 1;
