@@ -172,9 +172,12 @@ struct klsh_ctx {
   // KLSH_GRID_HINTS=1: size the big-run grids from the previous iteration's run counts.  Off by
   // default: measured slower on C2 (346 -> 370 ms; with fewer pending big-run workgroups the
   // small-run waves take the CUs the big runs need).
-  bool grid_hints = [] {
+  // KLSH_GRID_HINTS: 1 = every big-run class, 2 = the two rarest (>384, >896 rows), 0 (default) =
+  // none.  Measured: all hints 346 -> 370 ms on C2; the rare-class hints neutral on C2/C5 but
+  // 3.42 -> 6.25 s on C4, whose >896-row runs are the critical path.
+  int grid_hints = [] {
     const char* e = getenv("KLSH_GRID_HINTS");
-    return e && e[0] == '1';
+    return e ? atoi(e) : 0;
   }();
 
   ~klsh_ctx() { release(); }
@@ -461,14 +464,17 @@ klsh_ctx* klsh_create(int device, int* err) {
   }
   klsh_ctx* c = new klsh_ctx();
   c->device = device;
-  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
-  for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
-  // the big-run merge stream gets the highest priority: its workgroups need a whole CU's LDS and
-  // would otherwise wait behind the small-run waves (KLSH_BIG_PRIORITY=0: all equal)
+  // The big-run merge streams (aux 0 and the main stream, which carries the >384-row and
+  // >896-row runs) get the highest priority: their workgroups need most of a CU's LDS and would
+  // otherwise wait behind the small-run waves — on C4, where the >896-row runs are the critical
+  // path, a normal-priority main stream doubled their time (KLSH_BIG_PRIORITY=0: all equal)
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   const char* bp = getenv("KLSH_BIG_PRIORITY");
   const bool big_prio = !(bp && bp[0] == '0');
+  bool ok = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking,
+                                        big_prio ? prio_hi : prio_lo) == hipSuccess;
+  for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
   for (int i = 0; i < klsh::kMergeStreams; ++i) {
     ok = ok && hipStreamCreateWithPriority(&c->mw.aux[i], hipStreamNonBlocking,
                                            (i == 0 && big_prio) ? prio_hi : prio_lo) == hipSuccess;
@@ -784,13 +790,12 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
     if (int e = merge_nested(ctx, fk, fv, n, thr, over, seed_base, rng_counter, out, st))
       return e;
   }
-  if (ctx->grid_hints) {
+  if (ctx->grid_hints == 1) {
     memcpy(ctx->mw.hint, next_hint, sizeof(next_hint));
     ctx->mw.hint_small = next_small;
-  } else {
-    // always for the two rarest, most LDS-hungry classes (>384 rows: 142 KB, >896 rows: 64+ KB
-    // per workgroup): sized for the worst case, their mostly empty workgroups queue for whole CUs
-    // behind the other merge kernels and hold up the join (C2: 205 us per empty k_merge_huge)
+  } else if (ctx->grid_hints == 2) {
+    // the two rarest, most LDS-hungry classes (>384 rows: 142 KB, >896 rows: 64+ KB per
+    // workgroup) only
     ctx->mw.hint[2] = next_hint[2];
     ctx->mw.hint[klsh::kBigClasses] = next_hint[klsh::kBigClasses];
   }
