@@ -267,6 +267,15 @@ def main():
                  "frac": round(valu_achieved / VALU_PEAK_TFLOPS, 4),
                  "note": "separate f32 mul+add (no FMA: bit-exact with the reference), packed"},
     }
+    # the whole loop against HBM, SURVEY.md §8(d): B_t = N_t (8d + 16) + M_t (4d + 8) bytes per
+    # iteration (rows read by the projection and by the merge, keys and order written and read;
+    # per merge the new row and a member link), summed over the timed steps
+    loop_bytes = agg["sum_rows"] * (8 * d + 16) + agg["sum_merges"] * (4 * d + 8)
+    loop_gbs = loop_bytes / elapsed / 1e9
+    roofline["loop"] = {"achieved": round(loop_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(loop_gbs / HBM_PEAK_GBS, 5),
+                        "bytes_per_step": loop_bytes / args.steps,
+                        "note": "SURVEY.md 8(d) algorithmic bytes of the whole loop / step time"}
     cpu = None
     if world == 1:
         try:
