@@ -209,6 +209,10 @@ constexpr bool kRowPrefetch = KLSH_ROW_PREFETCH != 0;
 #define KLSH_LAZY_META 1
 #endif
 constexpr bool kLazyMeta = KLSH_LAZY_META != 0;  // -DKLSH_LAZY_META=0: eager loads (A/B build)
+#ifndef KLSH_NORM_FROM_ROW
+#define KLSH_NORM_FROM_ROW 1
+#endif
+constexpr bool kNormFromRow = KLSH_NORM_FROM_ROW != 0;  // -DKLSH_NORM_FROM_ROW=0: read r.nrm
 
 template <int G, int D, class Prefetch>
 __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
@@ -226,7 +230,9 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
   [[maybe_unused]] uint64_t sp1 = 0, sp2 = 0, sp3 = 0;
   {
     const bool valid = g < b;
-    float nrm = valid ? r.nrm[slot] : 0.0f;
+    // the row's norm: recomputed from the row (the same sequential chain that made the cached
+    // value, distance.cc:33-34, so the same bits) instead of a random 4-B read of r.nrm
+    float nrm = (!kNormFromRow && valid) ? r.nrm[slot] : 0.0f;
     // member count / list ends: only a merge needs them, and most batches have none — they are
     // loaded after the pairwise decisions, by waves that found a matching pair (saves three
     // random 4-B reads per row, as much traffic as the row itself)
@@ -241,11 +247,17 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
     } else {
       stage_rows<D>(r.x, r.dp, slot, valid, lds);  // row of lane l -> LDS row l, coalesced
     }
-    float sq = __builtin_sqrtf(nrm);  // this row's sqrtf(|x|^2), distance.cc:37
     if constexpr (kRowPrefetch) prefetch();  // the next batch's row loads fly during this batch
     wave_lds_fence();
     float x[D];
     load_row<D>(myrow, x);
+    if constexpr (kNormFromRow) {
+      nrm = 0.0f;
+#pragma unroll
+      for (int k = 0; k < D; ++k) nrm = nrm + x[k] * x[k];
+      if (!valid) nrm = 0.0f;
+    }
+    float sq = __builtin_sqrtf(nrm);  // this row's sqrtf(|x|^2), distance.cc:37
     const uint32_t bmax = wave_max(b);
 #ifdef KLSH_MERGE_PROF
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -457,7 +469,19 @@ __device__ __forceinline__ void pair_batch(const uint2* __restrict__ list, uint3
     float dot = 0.0f;
 #pragma unroll
     for (int q = 0; q < D; ++q) dot = dot + x1[q] * x0[q];  // cosine(c[1], c[0]), in order
-    const float n0 = r.nrm[s0], n1 = r.nrm[s1];
+    float n0, n1;
+    if constexpr (kNormFromRow) {  // recomputed from the rows in registers (same chain, same bits)
+      n0 = 0.0f;
+      n1 = 0.0f;
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        n0 = n0 + x0[q] * x0[q];
+        n1 = n1 + x1[q] * x1[q];
+      }
+    } else {
+      n0 = r.nrm[s0];
+      n1 = r.nrm[s1];
+    }
     if (decide(dc, dot, __builtin_sqrtf(n1) * __builtin_sqrtf(n0))) {
       merged = true;
       const uint32_t ca = r.cnt[s1], cb = r.cnt[s0];  // current = row 1, candidate = row 0
@@ -734,7 +758,19 @@ __global__ __launch_bounds__(256) void k_merge_pair(const uint2* __restrict__ li
       float dot = 0.0f;
 #pragma unroll
       for (int q = 0; q < D; ++q) dot = dot + x1[q] * x0[q];  // cosine(c[1], c[0]), in order
-      const float n0 = r.nrm[s0], n1 = r.nrm[s1];
+      float n0, n1;
+    if constexpr (kNormFromRow) {  // recomputed from the rows in registers (same chain, same bits)
+      n0 = 0.0f;
+      n1 = 0.0f;
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        n0 = n0 + x0[q] * x0[q];
+        n1 = n1 + x1[q] * x1[q];
+      }
+    } else {
+      n0 = r.nrm[s0];
+      n1 = r.nrm[s1];
+    }
       if (decide(dc, dot, __builtin_sqrtf(n1) * __builtin_sqrtf(n0))) {
         merged = true;
         const uint32_t ca = r.cnt[s1], cb = r.cnt[s0];  // current = row 1, candidate = row 0
