@@ -196,7 +196,7 @@ struct klsh_ctx {
   // communication.  klsh_set_option(ctx, "shard_min_rows", n); 0 = always sharded.
   uint64_t shard_min_rows = [] {
     const char* e = getenv("KLSH_SHARD_MIN_ROWS");
-    return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)(1u << 19);
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)(1u << 21);
   }();
 
   int world() const { return comm ? comm->world : 1; }
@@ -312,7 +312,7 @@ struct klsh_ctx {
     if ((e = dalloc(&rows.x, s * dp_)) || (e = dalloc(&rows.nrm, s)) || (e = dalloc(&rows.cnt, s)) ||
         (e = dalloc(&rows.head, s)) || (e = dalloc(&rows.tail, s)) || (e = dalloc(&rows.nxt, m)) ||
         (e = dalloc(&order, s)) || (e = dalloc(&alt, s)) || (e = dalloc(&keys, s)) ||
-        (e = dalloc(&keys2, s)) || (e = dalloc(&nk1, s)) || (e = dalloc(&nk2, s)) ||
+        (e = dalloc(&keys2, s)) || (e = dalloc(&nk1, s + 64)) || (e = dalloc(&nk2, s)) ||
         (e = dalloc(&nv2, s)) ||
         (e = dalloc(&hist, klsh::sort_ws_words(s))) ||
         (e = dalloc(&tile_sums, klsh::scan_ws_words(s))) ||
@@ -1036,11 +1036,9 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
     }
 
     // 2. exchange (key, slot) pairs: stable partition by owner, all-to-all-v
-    uint32_t *dk = nullptr, *dv = nullptr;
-    klsh::launch_dest(ctx->keys, n_g, shift, ctx->owner, ctx->nk1, ctx->nk2, s);
-    klsh::radix_sort(ctx->nk1, ctx->nk2, ctx->nv2, ctx->keys2, n_g, 8, ctx->hist, ctx->tile_sums,
-                     ctx->ctr, &dk, &dv, s);
-    klsh::launch_pack_pairs(ctx->keys, ctx->order, dv, n_g, ctx->sbuf, s);
+    if (klsh::launch_partition(ctx->keys, ctx->order, n_g, shift, ctx->owner, W, ctx->nk1,
+                               ctx->tile_sums, ctx->ctr, ctx->sbuf, s))
+      return fail(KLSH_E_ARG, "partition: unsupported world size");
     KLSH_HIP(hipGetLastError());
     if (timed_comm([&] {
           return cm->alltoallv(ctx->sbuf, scnt.data(), soff.data(), ctx->rbuf, rcnt.data(),

@@ -196,6 +196,12 @@ void launch_bin_hist(const uint32_t* keys, uint32_t n, int shift, uint32_t nbins
 void launch_bin_split(const uint32_t* hist_all, int world, uint32_t nbins, uint64_t total,
                       uint32_t* owner, uint32_t* cntmat, hipStream_t s);
 // dest[i] = owner[keys[i] >> shift]; idx[i] = i.
+// Stable partition of (keys[i], slots[i]), i < n, by owner[keys[i] >> shift] (world <= 64)
+// into out, owner-major (out's owner blocks start at the exclusive prefix of the send counts).
+// counts: world * ceil(n / 4096) words of workspace.  Returns -1 for an unsupported world.
+int launch_partition(const uint32_t* keys, const uint32_t* slots, uint32_t n, int shift,
+                     const uint32_t* owner, int world, uint32_t* counts, uint32_t* tile_sums,
+                     Counters* ctr, uint2* out, hipStream_t s);
 void launch_dest(const uint32_t* keys, uint32_t n, int shift, const uint32_t* owner,
                  uint32_t* dest, uint32_t* idx, hipStream_t s);
 // out[i] = (keys[idx[i]], slots[idx[i]]).

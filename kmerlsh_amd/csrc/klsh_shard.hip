@@ -122,6 +122,112 @@ void launch_unpack_pairs(const uint2* in, uint32_t n, uint32_t* keys, uint32_t* 
   if (n) k_unpack_pairs<<<(n + 255) / 256, 256, 0, s>>>(in, n, keys, slots);
 }
 
+// Stable partition of (key, slot) by owning rank in one read pass + one scatter pass (replaces
+// the dest -> 8-bit radix sort -> pack sequence).  Tile = 4096 positions; wave w of a tile owns
+// the contiguous positions [w*1024, w*1024 + 1024), 64 at a time, so "tile-major, then wave, then
+// step, then lane" is position order.  counts[o * ntiles + tile] = pairs of owner o in the tile;
+// after an exclusive scan over that owner-major array they are the tile's output offsets.
+constexpr uint32_t kPartTile = 4096;
+
+// Lanes of the wave whose owner equals mine (owner < 64: six ballots).
+__device__ __forceinline__ uint64_t same_owner(uint32_t o, bool valid) {
+  uint64_t m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    const uint64_t on = __ballot(valid && ((o >> b) & 1u));
+    m &= ((o >> b) & 1u) ? on : ~on;
+  }
+  return valid ? m : 0ull;
+}
+
+__global__ __launch_bounds__(256) void k_part_count(const uint32_t* __restrict__ keys, uint32_t n,
+                                                    int shift, const uint32_t* __restrict__ owner,
+                                                    int world, uint32_t ntiles,
+                                                    uint32_t* __restrict__ counts) {
+  __shared__ uint32_t c[kMaxRanks];
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  if (t < (uint32_t)world) c[t] = 0u;
+  __syncthreads();
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t T0 = blockIdx.x * kPartTile;
+#pragma unroll 1
+  for (uint32_t k = 0; k < kPartTile / 256; ++k) {
+    const uint32_t i = T0 + k * 256u + t;
+    const bool v = i < n;
+    const uint32_t o = v ? owner[keys[i] >> shift] : 0u;
+    const uint64_t peers = same_owner(o, v);
+    if (v && (peers & below) == 0ull) atomicAdd(&c[o], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  if (t < (uint32_t)world) counts[(size_t)t * ntiles + blockIdx.x] = c[t];
+}
+
+__global__ __launch_bounds__(256) void k_part_scatter(const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ slots,
+                                                      uint32_t n, int shift,
+                                                      const uint32_t* __restrict__ owner,
+                                                      int world, uint32_t ntiles,
+                                                      const uint32_t* __restrict__ offs,
+                                                      uint2* __restrict__ out) {
+  __shared__ uint32_t run[4][kMaxRanks];  // per wave: its next output position per owner
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t base = blockIdx.x * kPartTile + wv * (kPartTile / 4);
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  constexpr uint32_t K = kPartTile / 256;
+  if (lane < (uint32_t)world) run[wv][lane] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  // pass 1: this wave's pairs per owner
+#pragma unroll 1
+  for (uint32_t k = 0; k < K; ++k) {
+    const uint32_t i = base + k * 64u + lane;
+    const bool v = i < n;
+    const uint32_t o = v ? owner[keys[i] >> shift] : 0u;
+    const uint64_t peers = same_owner(o, v);
+    if (v && (peers & below) == 0ull) run[wv][o] += (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  // the tile's offset per owner + the pairs of the waves before this one
+  uint32_t pre = 0u;
+  if (lane < (uint32_t)world) {
+    pre = offs[(size_t)lane * ntiles + blockIdx.x];
+    for (uint32_t w = 0; w < wv; ++w) pre += run[w][lane];
+  }
+  __syncthreads();
+  if (lane < (uint32_t)world) run[wv][lane] = pre;
+  __builtin_amdgcn_wave_barrier();
+  // pass 2: scatter in position order (the keys are re-read, from L2)
+#pragma unroll 1
+  for (uint32_t k = 0; k < K; ++k) {
+    const uint32_t i = base + k * 64u + lane;
+    const bool v = i < n;
+    const uint32_t key = v ? keys[i] : 0u;
+    const uint32_t slot = v ? slots[i] : 0u;
+    const uint32_t o = v ? owner[key >> shift] : 0u;
+    const uint64_t peers = same_owner(o, v);
+    const uint32_t at = v ? run[wv][o] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (v) {
+      out[at + (uint32_t)__popcll(peers & below)] = make_uint2(key, slot);
+      if ((peers & below) == 0ull) run[wv][o] = at + (uint32_t)__popcll(peers);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+int launch_partition(const uint32_t* keys, const uint32_t* slots, uint32_t n, int shift,
+                     const uint32_t* owner, int world, uint32_t* counts, uint32_t* tile_sums,
+                     Counters* ctr, uint2* out, hipStream_t s) {
+  if (n == 0) return 0;
+  if (world < 1 || world > 64) return -1;
+  const uint32_t ntiles = (n + kPartTile - 1) / kPartTile;
+  k_part_count<<<ntiles, 256, 0, s>>>(keys, n, shift, owner, world, ntiles, counts);
+  device_scan(SrcArray{counts}, DstExclusive{counts}, (uint32_t)world * ntiles, tile_sums,
+              &ctr->total, &ctr->err, s);
+  k_part_scatter<<<ntiles, 256, 0, s>>>(keys, slots, n, shift, owner, world, ntiles, counts, out);
+  return 0;
+}
+
 // ------------------------------------------------------------------------------- deltas -----
 // One thread per record word: consecutive lanes write consecutive words (and read one row).
 __global__ __launch_bounds__(256) void k_delta_pack(Rows r, const uint32_t* __restrict__ ds,
