@@ -1391,61 +1391,165 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
     __syncthreads();
     auto sqrt_at = [&](uint32_t a) { return in_lds ? lq[a] : __builtin_sqrtf(r.nrm[S[a]]); };
     uint32_t size = b, i = 1;
-    while (i < size) {  // block-uniform
-      const uint32_t si = S[i];
-      const float sqi = sqrt_at(i);
-      for (int k = (int)t * 4; k < dp; k += kHugeNT * 4)
-        *reinterpret_cast<float4*>(xi + k) =
-            *reinterpret_cast<const float4*>(r.x + (size_t)si * dp + k);
-      __syncthreads();
-      uint32_t found = 0xFFFFFFFFu;
-      for (uint32_t c0 = 0; c0 < i; c0 += kHugeNT) {  // the first j < i that matches
-        const uint32_t j = c0 + t;
-        bool ok = false;
-        if (j < i) {
-          const uint32_t sj = S[j];
-          ok = decide(dc, dot_seq<D>(xi, r.x + (size_t)sj * dp, d), sqi * sqrt_at(j));
+    if constexpr (D > 0) {
+      // KB visited rows at once: positions i .. i+kc-1 are tested against every position below
+      // them in one pass over the run (each candidate row j loaded once for KB dot products).
+      // Until some candidate matches, the walk would visit exactly these rows in this order with
+      // nothing changed, so the first candidate a* with a match (smallest j) is the reference's
+      // next merge and the candidates before it simply advance i; the ones after it are
+      // re-tested next pass.  A hit of candidate 0 ends the pass at its chunk (as the one-row walk
+      // did), so merge-dense runs pay no extra chunks.
+      constexpr int KB = D <= 32 ? 8 : 4;
+      float* xk = xi;                          // [KB][dp] candidate rows
+      float* sqk = xk + KB * dp;               // [KB] their sqrtf(norms)
+      uint32_t* wk = reinterpret_cast<uint32_t*>(sqk + KB);  // [KB][NW] per-wave first hits
+      while (i < size) {  // block-uniform
+        const uint32_t kc = min((uint32_t)KB, size - i);
+        for (uint32_t q = t; q < kc * (uint32_t)(D / 4); q += kHugeNT) {
+          const uint32_t a = q / (D / 4), k4 = q % (D / 4);
+          *reinterpret_cast<float4*>(xk + a * dp + 4 * k4) =
+              *reinterpret_cast<const float4*>(r.x + (size_t)S[i + a] * dp + 4 * k4);
         }
-        const uint64_t m = __ballot(ok);
-        if (lane == 0)
-          wmin[par][wv] = m ? c0 + wv * 64u + (uint32_t)(__ffsll((unsigned long long)m) - 1)
-                            : 0xFFFFFFFFu;
+        if (t < kc) sqk[t] = sqrt_at(i + t);
         __syncthreads();
-        uint32_t best = 0xFFFFFFFFu;
+        uint32_t first[KB];  // this wave's first hit per candidate (wave-uniform)
 #pragma unroll
-        for (int q = 0; q < NW; ++q) best = min(best, wmin[par][q]);
-        par ^= 1u;
-        if (best != 0xFFFFFFFFu) {  // block-uniform
-          found = best;
-          break;
+        for (int a = 0; a < KB; ++a) first[a] = 0xFFFFFFFFu;
+        const uint32_t jend = i + kc - 1;  // candidate a tests positions j < i + a
+        for (uint32_t c0 = 0; c0 < jend; c0 += kHugeNT) {
+          const uint32_t j = c0 + t;
+          bool ok[KB];
+#pragma unroll
+          for (int a = 0; a < KB; ++a) ok[a] = false;
+          if (j < jend) {
+            float xj[D];
+            load_row<D>(r.x + (size_t)S[j] * dp, xj);
+            const float sqj = sqrt_at(j);
+#pragma unroll
+            for (int a = 0; a < KB; ++a)
+              if ((uint32_t)a < kc && j < i + (uint32_t)a)
+                ok[a] = decide(dc, dot_reg_lds<D>(xj, xk + a * dp), sqk[a] * sqj);
+          }
+#pragma unroll
+          for (int a = 0; a < KB; ++a) {
+            const uint64_t m = __ballot(ok[a]);
+            if (m && first[a] == 0xFFFFFFFFu)
+              first[a] = c0 + wv * 64u + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+          }
+          if (lane == 0) wmin[par][wv] = first[0];
+          __syncthreads();
+          bool hit0 = false;
+#pragma unroll
+          for (int q = 0; q < NW; ++q) hit0 = hit0 || wmin[par][q] != 0xFFFFFFFFu;
+          par ^= 1u;
+          if (hit0) break;  // block-uniform
         }
+        if (lane < (uint32_t)KB) {
+          uint32_t v = 0xFFFFFFFFu;
+#pragma unroll
+          for (int a = 0; a < KB; ++a)
+            if (lane == (uint32_t)a) v = first[a];
+          wk[lane * NW + wv] = v;
+        }
+        __syncthreads();
+        uint32_t astar = 0xFFFFFFFFu, found = 0xFFFFFFFFu;
+        for (uint32_t a = 0; a < kc && astar == 0xFFFFFFFFu; ++a) {
+          uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+          for (int q = 0; q < NW; ++q) best = min(best, wk[a * NW + q]);
+          if (best != 0xFFFFFFFFu) {
+            astar = a;
+            found = best;
+          }
+        }
+        __syncthreads();  // wk and xk are rewritten by the next pass
+        if (astar == 0xFFFFFFFFu) {
+          i += kc;
+          continue;
+        }
+        i += astar;
+        float* xa = xk + astar * dp;
+        const uint32_t si = S[i];
+        // c[j] = SetConsensus(c[i], c[j]); c[i] = c[--size]  (cluster.cc:70-75)
+        const uint32_t sj = S[found];
+        const uint32_t ca = r.cnt[si], cb = r.cnt[sj];
+        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+        float* xj = r.x + (size_t)sj * dp;
+        for (int k = (int)t; k < d; k += kHugeNT) {
+          const float v = consensus(xa[k], fa, xj[k], fb, fn);
+          xa[k] = v;  // the new row, for its norm
+          xj[k] = v;
+        }
+        __syncthreads();  // the new row is in memory and in LDS
+        if (t == 0) {
+          const float nn = dot_seq<D>(xa, xa, d);  // distance.cc:33-34
+          r.nrm[sj] = nn;
+          if (in_lds) lq[found] = __builtin_sqrtf(nn);
+          link_members(r, si, sj);
+          mark_dirty(sj, w, ctr);
+          S[i] = S[size - 1];
+          if (in_lds) lq[i] = lq[size - 1];
+        }
+        __syncthreads();
+        --size;
       }
-      if (found == 0xFFFFFFFFu) {
-        ++i;
-        continue;
+    } else {
+      while (i < size) {  // block-uniform
+        const uint32_t si = S[i];
+        const float sqi = sqrt_at(i);
+        for (int k = (int)t * 4; k < dp; k += kHugeNT * 4)
+          *reinterpret_cast<float4*>(xi + k) =
+              *reinterpret_cast<const float4*>(r.x + (size_t)si * dp + k);
+        __syncthreads();
+        uint32_t found = 0xFFFFFFFFu;
+        for (uint32_t c0 = 0; c0 < i; c0 += kHugeNT) {  // the first j < i that matches
+          const uint32_t j = c0 + t;
+          bool ok = false;
+          if (j < i) {
+            const uint32_t sj = S[j];
+            ok = decide(dc, dot_seq<D>(xi, r.x + (size_t)sj * dp, d), sqi * sqrt_at(j));
+          }
+          const uint64_t m = __ballot(ok);
+          if (lane == 0)
+            wmin[par][wv] = m ? c0 + wv * 64u + (uint32_t)(__ffsll((unsigned long long)m) - 1)
+                              : 0xFFFFFFFFu;
+          __syncthreads();
+          uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+          for (int q = 0; q < NW; ++q) best = min(best, wmin[par][q]);
+          par ^= 1u;
+          if (best != 0xFFFFFFFFu) {  // block-uniform
+            found = best;
+            break;
+          }
+        }
+        if (found == 0xFFFFFFFFu) {
+          ++i;
+          continue;
+        }
+        // c[j] = SetConsensus(c[i], c[j]); c[i] = c[--size]  (cluster.cc:70-75)
+        const uint32_t sj = S[found];
+        const uint32_t ca = r.cnt[si], cb = r.cnt[sj];
+        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+        float* xj = r.x + (size_t)sj * dp;
+        for (int k = (int)t; k < d; k += kHugeNT) {
+          const float v = consensus(xi[k], fa, xj[k], fb, fn);
+          xi[k] = v;  // the new row, for its norm
+          xj[k] = v;
+        }
+        __syncthreads();  // the new row is in memory and in LDS
+        if (t == 0) {
+          const float nn = dot_seq<D>(xi, xi, d);  // distance.cc:33-34
+          r.nrm[sj] = nn;
+          if (in_lds) lq[found] = __builtin_sqrtf(nn);
+          link_members(r, si, sj);
+          mark_dirty(sj, w, ctr);
+          S[i] = S[size - 1];
+          if (in_lds) lq[i] = lq[size - 1];
+        }
+        __syncthreads();
+        --size;
       }
-      // c[j] = SetConsensus(c[i], c[j]); c[i] = c[--size]  (cluster.cc:70-75)
-      const uint32_t sj = S[found];
-      const uint32_t ca = r.cnt[si], cb = r.cnt[sj];
-      const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
-      float* xj = r.x + (size_t)sj * dp;
-      for (int k = (int)t; k < d; k += kHugeNT) {
-        const float v = consensus(xi[k], fa, xj[k], fb, fn);
-        xi[k] = v;  // the new row, for its norm
-        xj[k] = v;
-      }
-      __syncthreads();  // the new row is in memory and in LDS
-      if (t == 0) {
-        const float nn = dot_seq<D>(xi, xi, d);  // distance.cc:33-34
-        r.nrm[sj] = nn;
-        if (in_lds) lq[found] = __builtin_sqrtf(nn);
-        link_members(r, si, sj);
-        mark_dirty(sj, w, ctr);
-        S[i] = S[size - 1];
-        if (in_lds) lq[i] = lq[size - 1];
-      }
-      __syncthreads();
-      --size;
     }
     if (in_lds)
       for (uint32_t a = t; a < size; a += kHugeNT) slots[p + a] = ls[a];
@@ -1464,7 +1568,12 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
 
 static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, const Rows& r,
                         Counters* ctr, uint32_t n, hipStream_t s) {
-  const size_t lds = sizeof(uint32_t) * kHugeLdsRows * 2 + sizeof(float) * (size_t)r.dp;
+  // slots + sqrt norms, then up to 8 candidate rows + their norms + per-wave first hits
+  const bool batched = r.d == 8 || r.d == 16 || r.d == 32 || r.d == 64;
+  const size_t lds = sizeof(uint32_t) * kHugeLdsRows * 2 +
+                     (batched ? sizeof(float) * (size_t)r.dp * 8 + sizeof(float) * 8 +
+                                    sizeof(uint32_t) * 8 * (kHugeNT / 64)
+                              : sizeof(float) * (size_t)r.dp);
   static const bool lds_ok = [] {
     bool ok = true;
     for (const void* f : {reinterpret_cast<const void*>(&k_merge_huge<0>),
