@@ -781,6 +781,11 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
     small_batches += (ctx->h_ctr->n_cls[c] + per - 1) / per;
   }
   const uint32_t next_small = std::max<uint32_t>(2 * small_batches + 64, 256);
+  static const uint32_t big896_aux_min = [] {  // KLSH_BIG896_AUX_MIN: runs that move the class
+    const char* e = getenv("KLSH_BIG896_AUX_MIN");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 64u;
+  }();
+  ctx->mw.big896_aux = ctx->h_ctr->n_big[2] >= big896_aux_min ? 1u : 0u;
   if (ctx->h_ctr->n_over > 0) {
     std::vector<uint2> over;
     uint64_t hyp = 0;
@@ -910,8 +915,9 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     st->sum_merges += n - ctx->n_live;
     threshold -= sim_step;
     if (iter_log)
-      fprintf(iter_log, "%d %llu %d %.4f %.4f\n", it, (unsigned long long)n, h, now_ms() - t_it,
-              ctx->t_enqueued - t_it);
+      fprintf(iter_log, "%d %llu %d %.4f %.4f %u %u %u %u\n", it, (unsigned long long)n, h,
+              now_ms() - t_it, ctx->t_enqueued - t_it, ctx->h_ctr->n_big[0], ctx->h_ctr->n_big[1],
+              ctx->h_ctr->n_big[2], ctx->h_ctr->n_huge);
   }
   if (iter_log) fflush(iter_log);
   return 0;
@@ -1200,6 +1206,8 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   ctx->ctr_clean = false;
   ctx->spec_pending = false;
   ctx->mw.hint_small = 0;
+  // no run counts yet: only very large inputs start with the 385..896-row class on aux 2
+  ctx->mw.big896_aux = ctx->n_live >= (1u << 24) ? 1u : 0u;
   // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
   // lshash.cc:36-42), so repeated timed calls never reuse a previous call's tables.
   ctx->w_count = 0;

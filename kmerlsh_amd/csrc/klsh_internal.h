@@ -77,6 +77,9 @@ struct MergeWork {
   // is correct).
   uint32_t hint[kBigClasses + 1];
   uint32_t hint_small;  // the same for the fused small-run kernel (batches)
+  // 385..896-row runs on aux 2 instead of ahead of the >896-row runs on the main stream: set by
+  // the engine when the previous iteration had many of them (C4: thousands; C2: < 10)
+  uint32_t big896_aux;
   hipStream_t aux[3];
   hipEvent_t fork;
   hipEvent_t join[3];

@@ -1359,6 +1359,10 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
 // from memory, one exact sequential dot product each), and the first hit of the chunk is found
 // by a ballot + cross-wave min.  The run's slots and sqrtf(norms) live in LDS when they fit.
 constexpr int kHugeNT = 512;
+#ifndef KLSH_HUGE_KB
+#define KLSH_HUGE_KB 8
+#endif
+constexpr int kHugeKB = KLSH_HUGE_KB;  // visited rows tested per pass (half at d = 64)
 constexpr uint32_t kHugeLdsRows = 8192;
 
 template <int D>  // D: d at compile time (unrolled dots), 0 = any d
@@ -1399,7 +1403,7 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
       // next merge and the candidates before it simply advance i; the ones after it are
       // re-tested next pass.  A hit of candidate 0 ends the pass at its chunk (as the one-row walk
       // did), so merge-dense runs pay no extra chunks.
-      constexpr int KB = D <= 32 ? 8 : 4;
+      constexpr int KB = D <= 32 ? kHugeKB : kHugeKB / 2;
       float* xk = xi;                          // [KB][dp] candidate rows
       float* sqk = xk + KB * dp;               // [KB] their sqrtf(norms)
       uint32_t* wk = reinterpret_cast<uint32_t*>(sqk + KB);  // [KB][NW] per-wave first hits
@@ -1568,11 +1572,11 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
 
 static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, const Rows& r,
                         Counters* ctr, uint32_t n, hipStream_t s) {
-  // slots + sqrt norms, then up to 8 candidate rows + their norms + per-wave first hits
+  // slots + sqrt norms, then the candidate rows + their norms + per-wave first hits
   const bool batched = r.d == 8 || r.d == 16 || r.d == 32 || r.d == 64;
   const size_t lds = sizeof(uint32_t) * kHugeLdsRows * 2 +
-                     (batched ? sizeof(float) * (size_t)r.dp * 8 + sizeof(float) * 8 +
-                                    sizeof(uint32_t) * 8 * (kHugeNT / 64)
+                     (batched ? sizeof(float) * (size_t)r.dp * kHugeKB + sizeof(float) * kHugeKB +
+                                    sizeof(uint32_t) * kHugeKB * (kHugeNT / 64)
                               : sizeof(float) * (size_t)r.dp);
   static const bool lds_ok = [] {
     bool ok = true;
@@ -2033,7 +2037,12 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
     launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(0));
   else
     launch_big<D, 384, 256, false>(w, 1, slots, dc, r, ctr, n, f.lane(0));
-  launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
+  // many 385..896-row runs (w.big896_aux): they go on aux 2, ahead of the small runs, instead of
+  // in front of the >896-row runs on the main stream — serialised, the two long-walk classes
+  // make the main stream the critical path (C4 1794 -> 1432 ms); with a handful of them (C2)
+  // the main stream is the better place (measured 281-285 vs 284-294 ms)
+  launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n,
+                                 f.on ? (w.big896_aux ? f.lane(2) : s) : f.lane(0));
   launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   static const bool big128_wide = [] {  // KLSH_BIG128_NT=256: 4 waves per 65..128-row run (A/B)
     const char* e = getenv("KLSH_BIG128_NT");
