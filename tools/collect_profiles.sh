@@ -21,6 +21,8 @@ run c2_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c2
 run c2_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex k_project -d $out/c2_fetch -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline none
 run c2_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex k_project -d $out/c2_write -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline none
 if [ "$1" = all ]; then
+  run c4_bench 400 python bench.py --config c4 --steps 2 --warmup 1 --cpu-baseline none
+  run c5_bench 400 python bench.py --config c5 --steps 2 --warmup 1 --cpu-baseline none
   run c4_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c4_stats -o run -- python bench.py --config c4 --steps 1 --warmup 0 --cpu-baseline none
   run c5_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c5_stats -o run -- python bench.py --config c5 --steps 1 --warmup 0 --cpu-baseline none
 fi

@@ -34,9 +34,10 @@ for cfg in ("c2", "c4", "c5"):
     if s:
         shutil.copy(s, os.path.join(dst, f"{tag}_{cfg}_kernel_stats.csv"))
         stats_txt(s, os.path.join(dst, f"{tag}_{cfg}_kernel_stats.txt"))
-b = os.path.join(src, "c2_bench.log")
-if os.path.exists(b):
-    shutil.copy(b, os.path.join(dst, f"{tag}_c2_bench.log"))
+for cfg in ("c2", "c4", "c5"):
+    b = os.path.join(src, f"{cfg}_bench.log")
+    if os.path.exists(b):
+        shutil.copy(b, os.path.join(dst, f"{tag}_{cfg}_bench.log"))
 
 summary = {}
 vals = {}
