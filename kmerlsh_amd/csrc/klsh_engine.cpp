@@ -319,7 +319,8 @@ struct klsh_ctx {
         (e = dalloc(&mw.seg, s + 64)) || (e = dalloc(&mw.over, s + 64)) ||
         (e = dalloc(&pw.fix, s)) || (e = dalloc(&pw.ws, 64)) ||
         (e = dalloc(&mw.big[0], s / 65 + 64)) || (e = dalloc(&mw.big[1], s / 129 + 64)) ||
-        (e = dalloc(&mw.big[2], s / 385 + 64)) || (e = dalloc(&mw.huge, s / 897 + 64))) {
+        (e = dalloc(&mw.big[2], s / 193 + 64)) || (e = dalloc(&mw.big[3], s / 385 + 64)) ||
+        (e = dalloc(&mw.huge, s / 897 + 64))) {
       release_state();
       return e;
     }
@@ -785,7 +786,7 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
     const char* e = getenv("KLSH_BIG896_AUX_MIN");
     return e ? (uint32_t)strtoul(e, nullptr, 10) : 64u;
   }();
-  ctx->mw.big896_aux = ctx->h_ctr->n_big[2] >= big896_aux_min ? 1u : 0u;
+  ctx->mw.big896_aux = ctx->h_ctr->n_big[klsh::kBigClasses - 1] >= big896_aux_min ? 1u : 0u;
   if (ctx->h_ctr->n_over > 0) {
     std::vector<uint2> over;
     uint64_t hyp = 0;
@@ -801,7 +802,7 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
   } else if (ctx->grid_hints == 2) {
     // the two rarest, most LDS-hungry classes (>384 rows: 142 KB, >896 rows: 64+ KB per
     // workgroup) only
-    ctx->mw.hint[2] = next_hint[2];
+    ctx->mw.hint[klsh::kBigClasses - 1] = next_hint[klsh::kBigClasses - 1];
     ctx->mw.hint[klsh::kBigClasses] = next_hint[klsh::kBigClasses];
   }
   if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
@@ -917,7 +918,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     if (iter_log)
       fprintf(iter_log, "%d %llu %d %.4f %.4f %u %u %u %u\n", it, (unsigned long long)n, h,
               now_ms() - t_it, ctx->t_enqueued - t_it, ctx->h_ctr->n_big[0], ctx->h_ctr->n_big[1],
-              ctx->h_ctr->n_big[2], ctx->h_ctr->n_huge);
+              ctx->h_ctr->n_big[2] + ctx->h_ctr->n_big[3], ctx->h_ctr->n_huge);
   }
   if (iter_log) fflush(iter_log);
   return 0;

@@ -33,8 +33,10 @@ inline uint64_t scan_ws_words(uint64_t slots) {
 // Bucket runs of 65..896 rows are merged by one workgroup with the run's decision matrix in LDS
 // (k_merge_big; three size classes, rows in LDS up to 384); longer runs by one wave from memory
 // (k_merge_huge).
-constexpr int kBigClasses = 3;
-constexpr int kBigRows[kBigClasses] = {128, 384, 896};
+// 65..128, 129..192, 193..384, 385..896 rows: the 129..192 class has its own layout (62 KB of
+// LDS at d = 64) so two of its workgroups share a CU, where a 384-row layout needs 130 KB
+constexpr int kBigClasses = 4;
+constexpr int kBigRows[kBigClasses] = {128, 192, 384, 896};
 
 // Runs of 2..64 rows are merged by G-lane groups, one size class per G = 2, 4, ..., 64
 // (class c holds runs of 2^c < b <= 2^(c+1) rows).

@@ -189,7 +189,8 @@ __device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucke
   if (bucket_thr >= 0 && b > (uint32_t)bucket_thr) {  // cluster.cc:286 -> nestedCluster
     w.over[atomicAdd(&ctr->n_over, 1u)] = make_uint2(p, b);
   } else if (b <= (uint32_t)kBigRows[kBigClasses - 1]) {
-    const int c = b <= (uint32_t)kBigRows[0] ? 0 : b <= (uint32_t)kBigRows[1] ? 1 : 2;
+    int c = 0;
+    while (b > (uint32_t)kBigRows[c]) ++c;
     w.big[c][atomicAdd(&ctr->n_big[c], 1u)] = make_uint2(p, b);
   } else {
     w.huge[atomicAdd(&ctr->n_huge, 1u)] = make_uint2(p, b);
@@ -1310,7 +1311,7 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
 }
 
 template <int D, int RB, int NT, bool ROWS_LDS>
-__global__ __launch_bounds__(NT) void k_merge_big(const uint2* __restrict__ list, int cls,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RB == 192 ? 2 : 1))) void k_merge_big(const uint2* __restrict__ list, int cls,
                                                   uint32_t* __restrict__ slots, Decider dc,
                                                   Rows r, Counters* ctr, uint32_t* dlist) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1333,13 +1334,16 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
 #pragma unroll
     for (int c = 0; c < kBigClasses; ++c)
       cnt[c] = __hip_atomic_load(&ctr->n_big[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // one index space, 385..896 first, then 129..384, then 65..128
-    const uint32_t a2 = cnt[2], a1 = a2 + cnt[1], total = a1 + cnt[0];
+    // one index space, longest class first: 385..896, 193..384, 129..192, 65..128
+    const uint32_t a3 = cnt[3], a2 = a3 + cnt[2], a1 = a2 + cnt[1], total = a1 + cnt[0];
     for (uint32_t li = blockIdx.x; li < total; li += nbig) {  // block-uniform
-      if (li < a2)
-        big_runs<D, 896, 256, false>(w.big[2], 2, li + 1, li, 1u << 30, slots, dc, r, ctr, w.dlist, smem);
+      if (li < a3)
+        big_runs<D, 896, 256, false>(w.big[3], 3, li + 1, li, 1u << 30, slots, dc, r, ctr, w.dlist, smem);
+      else if (li < a2)
+        big_runs<D, 384, 256, true>(w.big[2], 2, li - a3 + 1, li - a3, 1u << 30, slots, dc, r, ctr,
+                                    w.dlist, smem);
       else if (li < a1)
-        big_runs<D, 384, 256, true>(w.big[1], 1, li - a2 + 1, li - a2, 1u << 30, slots, dc, r, ctr,
+        big_runs<D, 192, 256, true>(w.big[1], 1, li - a2 + 1, li - a2, 1u << 30, slots, dc, r, ctr,
                                     w.dlist, smem);
       else
         big_runs<D, 128, 256, true>(w.big[0], 0, li - a1 + 1, li - a1, 1u << 30, slots, dc, r, ctr,
@@ -1560,12 +1564,12 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
     for (uint32_t a = size + t; a < b; a += kHugeNT) slots[p + a] = kInvalid;
     __syncthreads();
     if (t == 0) {
-      MPROF_ADD(3, 0, 1);
-      MPROF_ADD(3, 1, b);
-      MPROF_ADD(3, 2, b - size);
-      MPROF_ADD(3, 4, MPROF_T() - pt0);
-      MPROF_MAX(3, 5, MPROF_T() - pt0);
-      MPROF_MAX(3, 6, b);
+      MPROF_ADD(kBigClasses, 0, 1);
+      MPROF_ADD(kBigClasses, 1, b);
+      MPROF_ADD(kBigClasses, 2, b - size);
+      MPROF_ADD(kBigClasses, 4, MPROF_T() - pt0);
+      MPROF_MAX(kBigClasses, 5, MPROF_T() - pt0);
+      MPROF_MAX(kBigClasses, 6, b);
     }
   }
 }
@@ -2018,9 +2022,10 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   if (n < tail_max && small_fused()) {
     using L896 = BigLayout<D, 896, false>;
     using L384 = BigLayout<D, 384, true>;
+    using L192 = BigLayout<D, 192, true>;
     using L128 = BigLayout<D, 128, true>;
     constexpr size_t small_lds = 4 * 64 * (D + 4) * sizeof(float);
-    constexpr size_t lds = std::max({L896::bytes, L384::bytes, L128::bytes, small_lds});
+    constexpr size_t lds = std::max({L896::bytes, L384::bytes, L192::bytes, L128::bytes, small_lds});
     static const bool lds_ok =
         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_tail<D>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
@@ -2034,20 +2039,22 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   // longest walks first on each stream; the longest runs (few, long walks) on the main stream,
   // concurrent with the auxiliary ones (it waits for them at the join)
   if (big384_rows_lds())
-    launch_big<D, 384, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(0));
+    launch_big<D, 384, 256, true>(w, 2, slots, dc, r, ctr, n, f.lane(0));
   else
-    launch_big<D, 384, 256, false>(w, 1, slots, dc, r, ctr, n, f.lane(0));
+    launch_big<D, 384, 256, false>(w, 2, slots, dc, r, ctr, n, f.lane(0));
   // many 385..896-row runs (w.big896_aux): they go on aux 2, ahead of the small runs, instead of
   // in front of the >896-row runs on the main stream — serialised, the two long-walk classes
   // make the main stream the critical path (C4 1794 -> 1432 ms); with a handful of them (C2)
   // the main stream is the better place (measured 281-285 vs 284-294 ms)
-  launch_big<D, 896, 256, false>(w, 2, slots, dc, r, ctr, n,
+  launch_big<D, 896, 256, false>(w, 3, slots, dc, r, ctr, n,
                                  f.on ? (w.big896_aux ? f.lane(2) : s) : f.lane(0));
   launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   static const bool big128_wide = [] {  // KLSH_BIG128_NT=256: 4 waves per 65..128-row run (A/B)
     const char* e = getenv("KLSH_BIG128_NT");
     return e && atoi(e) == 256;
   }();
+  // 129..192 rows: two workgroups per CU (62 KB of LDS at d = 64), ahead of 65..128 on aux 1
+  launch_big<D, 192, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(1));
   if (big128_wide)
     launch_big<D, 128, 256, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   else
@@ -2098,8 +2105,9 @@ static void launch_groups_wide(const Rows& r, const uint32_t* seg, uint32_t hi, 
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
   const Fork f(w, s);
-  launch_big_wide<384, 256, 32>(w, 1, slots, dc, r, ctr, n, f.lane(0));
-  launch_big_wide<896, 256, 16>(w, 2, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
+  launch_big_wide<384, 256, 32>(w, 2, slots, dc, r, ctr, n, f.lane(0));
+  launch_big_wide<384, 256, 32>(w, 1, slots, dc, r, ctr, n, f.lane(0));  // 129..192 rows
+  launch_big_wide<896, 256, 16>(w, 3, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   k_merge_group_wide<64><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
@@ -2134,8 +2142,8 @@ void merge_prof_dump(FILE* f) {
 #ifdef KLSH_MERGE_PROF
   unsigned long long h[8][8];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mprof), sizeof(h)) != hipSuccess) return;
-  const char* names[4] = {"big128", "big384", "big896", "huge"};
-  for (int c = 0; c < 4; ++c)
+  const char* names[kBigClasses + 1] = {"big128", "big192", "big384", "big896", "huge"};
+  for (int c = 0; c <= kBigClasses; ++c)
     if (h[c][0])
       fprintf(f, "[mprof] %-7s runs %8llu rows %10llu merges %9llu  load+tiles %9.3f ms  walk %9.3f ms"
                  "  (per run %7.2f + %7.2f us)  max run %8.2f us  max b %llu\n",
@@ -2143,7 +2151,7 @@ void merge_prof_dump(FILE* f) {
               h[c][3] * 1e-2 / h[c][0], h[c][4] * 1e-2 / h[c][0], h[c][5] * 1e-2, h[c][6]);
   unsigned long long wpf[8][8];
   if (hipMemcpyFromSymbol(wpf, HIP_SYMBOL(g_wprof), sizeof(wpf)) == hipSuccess)
-    for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < kBigClasses; ++c)
       if (wpf[c][4])
         fprintf(f, "[wprof] %-7s steps %9llu  clocks/step: find %7.0f  select+consensus %7.0f"
                    "  dots %7.0f  bits %7.0f   find rounds/step %.2f\n",

@@ -167,6 +167,9 @@ def test_pcluster_matches_reference(engine, name):
     # > 896 rows (k_merge_huge, batched candidates): merge-sparse and merge-dense walks
     (3000, 32, 100, 0.05, 0.9), (2500, 64, 300, 0.08, 0.85), (1500, 16, 20, 0.03, 0.95),
     (4000, 8, 400, 0.1, 0.8), (1200, 32, 1200, 0.3, 0.99), (2000, 64, 2, 0.01, 0.9),
+    # the 129..192 / 193..384 class boundary (two workgroups per CU below it)
+    (192, 64, 15, 0.05, 0.9), (193, 64, 15, 0.05, 0.9), (160, 32, 1, 0.0, 0.9), (190, 16, 12, 0.1, 0.85),
+    (180, 130, 12, 0.05, 0.9),
 ])
 def test_pcluster_run_lengths_vs_oracle(engine, oracle, b, d, groups, noise, thr):
     """Every merge path by bucket length: G-lane groups (<= 64), LDS matrix (65..384), wave (> 384)."""
