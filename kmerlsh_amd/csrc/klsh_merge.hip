@@ -1311,7 +1311,7 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
 }
 
 template <int D, int RB, int NT, bool ROWS_LDS>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RB == 192 ? 2 : 1))) void k_merge_big(const uint2* __restrict__ list, int cls,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RB <= 192 ? 2 : 1))) void k_merge_big(const uint2* __restrict__ list, int cls,
                                                   uint32_t* __restrict__ slots, Decider dc,
                                                   Rows r, Counters* ctr, uint32_t* dlist) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2053,7 +2053,8 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
     const char* e = getenv("KLSH_BIG128_NT");
     return e && atoi(e) == 256;
   }();
-  // 129..192 rows: two workgroups per CU (62 KB of LDS at d = 64), ahead of 65..128 on aux 1
+  // 129..192 rows: two workgroups per CU (62 KB of LDS at d = 64, VGPRs capped at 256 like the
+  // 65..128 class), ahead of 65..128 on aux 1
   launch_big<D, 192, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(1));
   if (big128_wide)
     launch_big<D, 128, 256, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
