@@ -465,7 +465,10 @@ __global__ __launch_bounds__(256) void k_project_mfma(const float* __restrict__ 
 // streamed 64 columns at a time (8 loads in flight per lane).  The pairs the screen cannot call
 // (≈1 % at d = 512: the bound grows with d) go to a list that k_project_fix settles with the exact
 // sequential chains afterwards, one lane per pair — in-wave they would stall 31 other rows.
-__global__ __launch_bounds__(256) void k_project_mfma_wide(const float* __restrict__ X, int d, int dp,
+// Six waves per workgroup: the 64-KB fragment table is shared by 6 waves instead of 4, so two
+// workgroups per CU keep 12 waves (3 per SIMD at 144 VGPRs) of row loads in flight, not 8.
+constexpr int kWideNT = 384;
+__global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __restrict__ X, int d, int dp,
                                                            const uint32_t* __restrict__ slots,
                                                            uint32_t* __restrict__ keys, uint32_t n,
                                                            const float* __restrict__ W, int h,
@@ -476,7 +479,7 @@ __global__ __launch_bounds__(256) void k_project_mfma_wide(const float* __restri
   float* swn = reinterpret_cast<float*>(psm + (size_t)KS * 64 * 2 * sizeof(pbf16x8));  // [32]
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, r = lane & 31u, hh = lane >> 5;
   // hyperplane fragments: entry (s, L) = W[j = L&31][16s + 8(L>>5) + 0..7], split
-  for (int e = (int)t; e < KS * 64; e += 256) {
+  for (int e = (int)t; e < KS * 64; e += kWideNT) {
     const int sk = e >> 6, L = e & 63, j = L & 31, k0 = 16 * sk + 8 * (L >> 5);
     float x[8];
 #pragma unroll
@@ -502,8 +505,9 @@ __global__ __launch_bounds__(256) void k_project_mfma_wide(const float* __restri
   __syncthreads();
   const float wn = swn[r];
   const bool col_ok = (int)r < h;
-  const uint32_t step = gridDim.x * 128u;
-  for (uint32_t g0 = (blockIdx.x * 4u + wv) * 32u; g0 < n; g0 += step) {
+  constexpr uint32_t NWV = kWideNT / 64;
+  const uint32_t step = gridDim.x * NWV * 32u;
+  for (uint32_t g0 = (blockIdx.x * NWV + wv) * 32u; g0 < n; g0 += step) {
     const uint32_t row = g0 + r;
     const bool valid = row < n;
     const float* xr = X + (size_t)slots[valid ? row : g0] * dp;
@@ -682,9 +686,9 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
           hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_fix),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) == hipSuccess;
       (void)lds_ok;
-      const uint32_t groups = (n + 127) / 128;
+      const uint32_t groups = (n + kWideNT / 2 - 1) / (kWideNT / 2);  // 32 rows per wave
       const dim3 gm(std::min<uint32_t>(groups, 2048u));
-      k_project_mfma_wide<<<gm, block, lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or,
+      k_project_mfma_wide<<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or,
                                                  project_eps(r.d), *pw);
       k_project_fix<<<1024, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw);
       return;

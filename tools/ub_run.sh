@@ -1,6 +1,3 @@
 cd $GRAFT_REPO_ROOT
-for nb in "9469536 23" "4000000 22" "2000000 21"; do
-  set -- $nb
-  timeout -k 5 60 ./tools/ubench_sort $1 $2 30 || exit 1
-  KLSH_SORT_BIGTILE=1 timeout -k 5 60 ./tools/ubench_sort $1 $2 30 || exit 1
-done
+b() { timeout -k 5 250 python bench.py --steps 2 --warmup 1 --cpu-baseline none "$@" 2>gpurun_out/err.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(round(d['ms_per_step'],1), d['final_clusters'], r['frac'], round(r['avg_launch_ms']*1e3,1))"; }
+for i in 1 2; do echo new c5; b --config c5; echo old c5; KLSH_LIB=$PWD/kmerlsh_amd/lib_ab/libklsh_ab.so b --config c5; done
