@@ -39,12 +39,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_TFLOPS = 78.6  # packed f32 mul / add issue ceiling (see roofline["valu"])
 
 CONFIGS = {
-    # name: (kmers, samples, iterations, min_similarity, description)
-    "c1": (100_000, 8, 10, 0.80, "C1: 100K k-mers x 8 samples, -I 10 -N 0.80"),
-    "c2": (10_000_000, 64, 500, 0.80, "C2: 10M k-mers x 64 samples, -I 500 -N 0.80"),
-    "c4": (100_000_000, 32, 100, 0.80, "C4: 100M k-mers x 32 samples, -I 100 -N 0.80"),
-    "c5": (10_000_000, 512, 500, 0.80, "C5: 10M k-mers x 512 samples, -I 500 -N 0.80"),
+    # name: (kmers, samples, iterations, min_similarity, synth seed, description)
+    "c1": (100_000, 8, 10, 0.80, 1, "C1: 100K k-mers x 8 samples, -I 10 -N 0.80"),
+    "c2": (10_000_000, 64, 500, 0.80, 11, "C2: 10M k-mers x 64 samples, -I 500 -N 0.80"),
+    "c4": (100_000_000, 32, 100, 0.80, 13, "C4: 100M k-mers x 32 samples, -I 100 -N 0.80"),
+    "c5": (10_000_000, 512, 500, 0.80, 17, "C5: 10M k-mers x 512 samples, -I 500 -N 0.80"),
 }
+SEED_BASE = 12345  # hyperplane seeding convention
 
 
 def log(msg: str) -> None:
@@ -111,36 +112,46 @@ def timed(step, steps: int, warmup: int, world: int, local: int = 0, sync=device
 def prepare(eng, n, d, seed):
     """synth counts -> GPU convert -> init pass; returns (rng counter, kept rows, init stats)."""
     from kmerlsh_amd import _native
+    from kmerlsh_amd.io import v_kmers_from_coverage
 
     t0 = time.time()
     counts, cov = _native.synth_counts(n, d, seed=seed)
-    # kmer_count.log carries "%f" coverages; v_kmers = float(cov) / float(kmap_size)
-    cov_f = np.array([np.float32(float("%f" % c)) for c in cov], dtype=np.float32)
-    v_kmers = (cov_f / np.float32(n)).astype(np.float32)
+    v_kmers = v_kmers_from_coverage(cov, n)  # as the reference reads kmer_count.log
     log(f"synth {n}x{d} in {time.time() - t0:.1f}s")
     eng.load_counts(counts, v_kmers)
     del counts
     kept, _ = eng.count()
-    _, counter, st0 = eng.cluster(0.80, 1, 100_000, 12345, 0)  # init pass (app/kmerLSH.cc:323)
+    # init pass (app/kmerLSH.cc:323): one iteration at 0.95, bucket threshold 1e5
+    _, counter, st0 = eng.cluster(0.80, 1, 100_000, SEED_BASE, 0)
     eng.snapshot()
     log(f"init pass: {kept} -> {st0['n_final']} rows ({st0['wall_ms']:.1f} ms)")
     return counter, kept, st0
 
 
-def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter):
-    """Reference (oracle/_ref) or oracle port timed on this host over a bounded sample: the first
-    3 iterations of the same main loop on the same post-init rows (same threshold schedule)."""
+def state_at(eng, t, min_sim, iters, counter0):
+    """The loop's state at the start of iteration t (the engine stopped after t iterations)."""
+    eng.restore()
+    if t > 0:
+        eng.set_option("stop_after", t)
+        try:
+            eng.cluster(min_sim, iters, 1_000_000, SEED_BASE, counter0)
+        finally:
+            eng.set_option("stop_after", 0)
+    return eng.result()
+
+
+def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
+    """The reference (oracle/_ref/ref_harness: the reference's own Cluster(), compiled from its
+    sources) or the oracle port, timed on this host's cores over a bounded sample of the same
+    loop: one iteration from the loop's own state at t = 0, .1 I, .2 I, .4 I, .6 I, .9 I (the
+    engine provides the state).  Its per-row cost, interpolated in t and weighted by the loop's
+    N_t trace, estimates T_loop; value = N_0 * I / T_loop like the metric.  The sampled iteration
+    runs at the reference's first-iteration threshold 0.95 (Cluster() always starts there), not
+    at the schedule's value at t: fewer merges, so the estimate favours the CPU slightly."""
     if mode == "none":
         return None
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     threads = min(16, os.cpu_count() or 1)
-    k = 3
-    step = np.float32((np.float32(0.95) - np.float32(min_sim)) / np.float32(iters))
-    sample_min = float(np.float32(0.95) - np.float32(k) * step)
-    eng.restore()
-    rows, off, ids = eng.result()
-    desc = (f"first {k} of {iters} iterations of the main loop on the same post-init "
-            f"{rows.shape[0]}x{d} rows (threshold 0.95 falling by {float(step):.6g})")
     kind = None
     if mode in ("auto", "reference") and os.path.exists(harness):
         kind = "reference"
@@ -148,31 +159,68 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter):
         kind = "port"
     if kind is None:
         return None
-    if kind == "reference":
-        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
-            src = os.path.join(tmp, "rows.f32")
-            rows.astype("<f4").tofile(src)
-            off.astype("<u8").tofile(src + ".off")
-            ids.astype("<u8").tofile(src + ".ids")
-            env = dict(os.environ, OMP_THREAD_LIMIT=str(threads), OMP_NUM_THREADS=str(threads),
-                       KLSH_SEED="12345")
-            log(f"cpu baseline: reference harness, {threads} threads, {desc}")
-            out = subprocess.run([harness, "cluster_w", src, src + ".off", src + ".ids",
-                                  str(rows.shape[0]), str(d), repr(sample_min), str(k), "1000000",
-                                  os.path.join(tmp, "out")], env=env, check=True,
-                                 capture_output=True, text=True, timeout=900).stdout
-        m = re.findall(r"hash\+cluster takes \(secs\): ([0-9.eE+-]+)", out)
-        secs = float(m[-1])
-    else:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import klsh_oracle
+    trace = np.asarray(trace, dtype=np.float64)
+    ts = sorted({min(iters - 1, int(f * iters)) for f in (0.0, 0.1, 0.2, 0.4, 0.6, 0.9)})
+    cost, secs_all = [], 0.0
+    for t in ts:
+        rows, off, ids = state_at(eng, t, min_sim, iters, counter0)
+        n_t = rows.shape[0]
+        if kind == "reference":
+            with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
+                src = os.path.join(tmp, "rows.f32")
+                rows.astype("<f4").tofile(src)
+                off.astype("<u8").tofile(src + ".off")
+                ids.astype("<u8").tofile(src + ".ids")
+                del rows, off, ids
+                env = dict(os.environ, OMP_THREAD_LIMIT=str(threads), OMP_NUM_THREADS=str(threads),
+                           KLSH_REF_THREADS=str(threads), KLSH_SEED=str(SEED_BASE))
+                out = subprocess.run([harness, "cluster_w", src, src + ".off", src + ".ids",
+                                      str(n_t), str(d), repr(float(min_sim)), "1", "1000000",
+                                      os.path.join(tmp, "out")], env=env, check=True,
+                                     capture_output=True, text=True, timeout=900).stdout
+            secs = float(re.findall(r"hash\+cluster takes \(secs\): ([0-9.eE+-]+)", out)[-1])
+        else:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import klsh_oracle
 
-        log(f"cpu baseline: oracle port, {threads} threads, {desc}")
-        t0 = time.perf_counter()
-        klsh_oracle.cluster(rows, sample_min, k, 1_000_000, 12345, counter, off, ids, threads)
-        secs = time.perf_counter() - t0
-    return {"value": n0 * k / secs, "unit": "k-mers·iterations/s", "cores": threads,
-            "kind": kind, "sample": desc, "seconds": secs}
+            t0 = time.perf_counter()
+            klsh_oracle.cluster(rows, float(min_sim), 1, 1_000_000, SEED_BASE, 0, off, ids, threads)
+            secs = time.perf_counter() - t0
+        log(f"cpu baseline ({kind}, {threads} threads): t={t} N_t={n_t}: {secs:.2f} s")
+        secs_all += secs
+        cost.append(secs / max(1, n_t))
+    per_row = np.interp(np.arange(len(trace)), ts, cost)
+    t_loop = float((trace * per_row).sum())
+    return {"value": n0 * iters / t_loop, "unit": "k-mers·iterations/s", "cores": threads,
+            "kind": kind, "estimated_loop_s": round(t_loop, 2), "sample_seconds": round(secs_all, 2),
+            "sample": (f"one iteration of the main loop from its own state at t = "
+                       f"{', '.join(map(str, ts))} of {iters} ({threads} threads, threshold 0.95); "
+                       f"per-row cost interpolated in t and weighted by the loop's N_t trace "
+                       f"(sum N_t = {int(trace.sum())}) to estimate T_loop")}
+
+
+def check_parity(config, trace, counter, result):
+    """Compare the last timed step with the committed full-size fixture (tests/golden/
+    fullsize_<config>.json: the oracle's — for C1/C2 also the reference CLI's — run of the same
+    workload).  Full loops: trace, rng counter and result md5s; pinned prefixes: the trace."""
+    import hashlib
+
+    path = os.path.join(ROOT, "tests", "golden", f"fullsize_{config}.json")
+    if not os.path.exists(path):
+        return {"checked": False}
+    with open(path) as f:
+        fx = json.load(f)
+    k = fx["run_iterations"]
+    out = {"checked": True, "fixture": os.path.relpath(path, ROOT), "iterations_pinned": k,
+           "trace": [int(v) for v in trace[:k]] == fx["trace"]}
+    if k == fx["iterations"]:
+        rows, off, ids = result()
+        md5 = lambda a: hashlib.md5(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+        out["counter"] = counter == fx["counter"]
+        out["md5"] = (md5(rows) == fx["md5_rows"] and md5(off) == fx["md5_offsets"] and
+                      md5(ids) == fx["md5_ids"])
+    out["ok"] = all(v for key, v in out.items() if key in ("trace", "counter", "md5"))
+    return out
 
 
 def pmc_traffic(config):
@@ -207,7 +255,7 @@ def main():
     world, rank, local = dist_setup()
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
-    n0, d, iters, min_sim, desc = CONFIGS[args.config]
+    n0, d, iters, min_sim, synth_seed, desc = CONFIGS[args.config]
     if args.iterations:
         iters = args.iterations
         desc += f" [profiling override: -I {iters}]"
@@ -224,18 +272,24 @@ def main():
         log(f"rank {rank}/{world}: RCCL group up")
     elif args.shard1:
         _native.comm_init_local([eng])
-    counter0, kept, _ = prepare(eng, n0, d, seed=11 if sharded else 11 + rank)
+    counter0, kept, _ = prepare(eng, n0, d, seed=synth_seed if sharded else synth_seed + rank)
 
     def step():
         eng.restore()
-        _, _, st = eng.cluster(min_sim, iters, 1_000_000, 12345, counter0)
-        return st
+        return eng.cluster(min_sim, iters, 1_000_000, SEED_BASE, counter0)
 
-    elapsed, stats = timed(step, args.steps, args.warmup, world, local)
+    elapsed, results = timed(step, args.steps, args.warmup, world, local)
     log(f"{args.steps} timed steps: {elapsed:.3f} s (max over {world} ranks)")
+    stats = [r[2] for r in results]
+    trace, counter = results[-1][0], results[-1][1]
 
     if rank != 0:
         return
+    # outside the timed region: the last step's output against the committed full-size fixture
+    parity = (check_parity(args.config, trace, counter, eng.result)
+              if (world == 1 or sharded) and not args.iterations else {"checked": False})
+    if parity.get("checked"):
+        log(f"parity vs {parity['fixture']}: {'ok' if parity['ok'] else 'MISMATCH'}")
     value = (1 if sharded else world) * n0 * iters * args.steps / elapsed
     agg = {k: sum(s[k] for s in stats) for k in stats[0]}
     phases = {p: agg[p + "_ms"] / args.steps
@@ -279,7 +333,7 @@ def main():
     cpu = None
     if world == 1:
         try:
-            cpu = cpu_baseline(eng, args.cpu_baseline, n0, d, iters, min_sim, counter0)
+            cpu = cpu_baseline(eng, args.cpu_baseline, n0, d, iters, min_sim, counter0, trace)
         except Exception as e:  # the baseline is reported, never required
             log(f"cpu baseline failed: {e}")
     line = {
@@ -296,8 +350,9 @@ def main():
         "scaling": "strong" if args.mode == "sharded" else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": (f"synthetic klsh-synth v1 (seed 11), {kept} rows kept of {n0}" if world == 1 or sharded
-                 else f"synthetic klsh-synth v1 (seed 11+rank), {kept} rows kept of {n0} per rank"),
+        "data": (f"synthetic klsh-synth v1 (seed {synth_seed}), {kept} rows kept of {n0}"
+                 if world == 1 or sharded else
+                 f"synthetic klsh-synth v1 (seed {synth_seed}+rank), {kept} rows kept of {n0} per rank"),
         "config": {"workload": desc + " (main Cluster loop after the init pass)", "kmers": n0,
                    "samples": d, "iterations": iters, "min_similarity": min_sim,
                    "bucket_size_threshold": 1_000_000,
@@ -309,8 +364,11 @@ def main():
         "rows_projected_per_step": agg["sum_rows"] / args.steps,
         "final_clusters": stats[-1]["n_final"],
         "nested_calls_per_step": agg["nested_calls"] / args.steps,
+        "parity": parity,
     }
     print(json.dumps(line), flush=True)
+    if parity.get("checked") and not parity["ok"]:
+        sys.exit(1)  # a fast wrong answer is not a result
 
 
 if __name__ == "__main__":

@@ -106,10 +106,11 @@ int klsh_comm_init(klsh_ctx* ctx, int rank, int world, const uint8_t* id /* 128 
  * klsh_cluster must then run on its own host thread, concurrently.  For tests on one GPU. */
 int klsh_comm_init_local(klsh_ctx** ctxs, int world);
 int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
-/* Tuning knobs: "shard_min_rows" (sharded loop: below this many live rows every rank runs the
- * remaining iterations on its own replica, without exchanges; default 524288, 0 = always
- * sharded), "phase_timing" (0/1: per-phase HIP events, adds latency).  Results never depend on
- * either. */
+/* Options: "shard_min_rows" (sharded loop: below this many live rows every rank runs the
+ * remaining iterations on its own replica, without exchanges; default 2097152 = 2^21, 0 = always
+ * sharded), "phase_timing" (0/1: per-phase HIP events, adds latency) — results never depend on
+ * either; "stop_after" (k > 0: klsh_cluster runs only the first k iterations of its threshold
+ * schedule, e.g. to pin a prefix of a long loop; 0 = all, the default). */
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
 
 /* ---- results ---------------------------------------------------------------------------------- */

@@ -199,6 +199,11 @@ struct klsh_ctx {
     return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)(1u << 21);
   }();
 
+  // "stop_after" (klsh_set_option): run only the first k iterations of a call's threshold
+  // schedule (0 = all).  Prefix parity tests of the long configs use it; results of the
+  // iterations that do run are unchanged.
+  int stop_after = 0;
+
   int world() const { return comm ? comm->world : 1; }
   int rank() const { return comm ? comm->rank : 0; }
 
@@ -937,7 +942,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
 // then local order: a small allgather of (runs, hyperplanes) gives each rank its RNG offset.
 // Member links are written only by the rank that merged them; the end of the call combines them
 // with an element-wise min (an unwritten link is kNil = 0xFFFFFFFF) and gathers the global order.
-static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
+static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations, int run_iters,
                            int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
                            uint64_t* nt_trace, klsh_stats* st) {
   klsh::Comm* cm = ctx->comm;
@@ -984,7 +989,7 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
   std::vector<size_t> scnt(W), soff(W), rcnt(W), roff(W), dcnt(W), doff(W);
 
   bool replicated = false;
-  for (int it = 0; it < iterations; ++it) {
+  for (int it = 0; it < run_iters; ++it) {
     if (N < ctx->shard_min_rows) {  // the replicated tail: every rank runs the rest on its own
       std::vector<size_t> cnt(W), off(W);
       size_t acc = 0;
@@ -998,7 +1003,7 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations,
       std::swap(ctx->order, ctx->alt);
       ctx->n_live = N;
       replicated = true;
-      if (int e = run_single(ctx, threshold, sim_step, it, iterations, bucket_size_threshold,
+      if (int e = run_single(ctx, threshold, sim_step, it, run_iters, bucket_size_threshold,
                              seed_base, rng_counter, nt_trace, st))
         return e;
       N = ctx->n_live;
@@ -1193,9 +1198,10 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   klsh_stats* st = stats ? stats : &local;
   memset(st, 0, sizeof(*st));
   st->world = (uint64_t)ctx->world();
+  const int run_iters = ctx->stop_after > 0 ? std::min(iterations, ctx->stop_after) : iterations;
   if (ctx->comm)  // any bound group, world 1 included (measures the sharded machinery alone)
-    return cluster_sharded(ctx, min_similarity, iterations, bucket_size_threshold, seed_base,
-                           rng_counter, nt_trace, st);
+    return cluster_sharded(ctx, min_similarity, iterations, run_iters, bucket_size_threshold,
+                           seed_base, rng_counter, nt_trace, st);
   const double t_start = now_ms();
 
   // cluster.cc:190-192 (all float)
@@ -1220,9 +1226,12 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
       return e;
   }
 
-  if (int e = run_single(ctx, threshold, sim_step, 0, iterations, bucket_size_threshold, seed_base,
+  if (int e = run_single(ctx, threshold, sim_step, 0, run_iters, bucket_size_threshold, seed_base,
                          rng_counter, nt_trace, st))
     return e;
+  // The survivor counters are published by the compaction's last workgroup, which need not be
+  // the last to finish writing ctx->order: drain the stream before klsh_count/klsh_result read it.
+  KLSH_HIP(hipStreamSynchronize(ctx->stream));
   st->n_final = ctx->n_live;
   st->wall_ms = now_ms() - t_start;
   if (getenv("KLSH_MERGE_PROF")) klsh::merge_prof_dump(stderr);
@@ -1273,6 +1282,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   }
   if (n == "phase_timing") {
     ctx->phase_timing = value != 0;
+    return 0;
+  }
+  if (n == "stop_after") {
+    if (value < 0 || value > INT32_MAX) return fail(KLSH_E_ARG, "stop_after must be in [0, 2^31)");
+    ctx->stop_after = (int)value;
     return 0;
   }
   return fail(KLSH_E_ARG, "unknown option " + n);
@@ -1447,7 +1461,10 @@ int klsh_pcluster(klsh_ctx* ctx, float thr) {
   KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
   KLSH_HIP(hipMemsetAsync(ctx->keys, 0, 4ull * n, s));  // one bucket: every key equal
   uint64_t dummy = 0;
-  return merge_and_compact(ctx, ctx->keys, ctx->order, n, thr, -1, 0, &dummy, nullptr, false);
+  if (int e = merge_and_compact(ctx, ctx->keys, ctx->order, n, thr, -1, 0, &dummy, nullptr, false))
+    return e;
+  KLSH_HIP(hipStreamSynchronize(s));  // see klsh_cluster: the order may still be in flight
+  return 0;
 }
 
 int klsh_hyperplanes(uint32_t seed_base, uint64_t* rng_counter, int h, int d, float* table) {

@@ -28,6 +28,14 @@ def read_count_log(path: str, d: int) -> tuple[int, np.ndarray]:
     return kmap, (cov / np.float32(kmap)).astype(np.float32)
 
 
+def v_kmers_from_coverage(coverage, kmap_size: int) -> np.ndarray:
+    """v_kmers[j] exactly as the reference derives it from kmer_count.log: the coverage is
+    written with "%f" (io/ioHT.cc:185), read back as float and divided by kmap_size in
+    float (app/kmerLSH.cc:471-482)."""
+    cov = np.array([np.float32(float("%f" % c)) for c in coverage], dtype=np.float32)
+    return (cov / np.float32(kmap_size)).astype(np.float32)
+
+
 def write_count_files(directory: str, counts: np.ndarray, coverage: np.ndarray) -> None:
     """kmer_count.bin/.log + a.txt/b.txt (d/2 samples each) for a (d, n) count matrix."""
     import os

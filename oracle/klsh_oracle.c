@@ -299,6 +299,13 @@ static uint64_t nested_cluster(klsh_oracle_state* st, uint32_t* s, uint64_t b, f
 int klsh_oracle_cluster(klsh_oracle_state* st, float min_similarity, int iters,
                         int bucket_size_threshold, klsh_oracle_rng* rng, uint64_t* nt_trace,
                         int nthreads) {
+  return klsh_oracle_cluster_prefix(st, min_similarity, iters, iters, bucket_size_threshold, rng,
+                                    nt_trace, nthreads);
+}
+
+int klsh_oracle_cluster_prefix(klsh_oracle_state* st, float min_similarity, int iters,
+                               int run_iters, int bucket_size_threshold, klsh_oracle_rng* rng,
+                               uint64_t* nt_trace, int nthreads) {
   const int d = st->d;
   const float max_similarity = 0.95f;
   const float sim_step = (max_similarity - min_similarity) / (float)iters;
@@ -309,7 +316,8 @@ int klsh_oracle_cluster(klsh_oracle_state* st, float min_similarity, int iters,
   (void)nthreads;
 #endif
   int it;
-  for (it = 0; it < iters; ++it) {
+  if (run_iters > iters) run_iters = iters;
+  for (it = 0; it < run_iters; ++it) {
     const uint64_t n = st->n;
     if (nt_trace) nt_trace[it] = n;
     if (n == 0) { /* reference aborts here (floor(log2(0)) -> size_t); we no-op */

@@ -62,6 +62,13 @@ int klsh_oracle_cluster(klsh_oracle_state* st, float min_similarity, int iters,
                         int bucket_size_threshold, klsh_oracle_rng* rng, uint64_t* nt_trace,
                         int nthreads);
 
+/* The first run_iters iterations of Cluster(..., iters, ...): the threshold schedule of an
+ * `iters`-iteration call (sim_step = (0.95 - min_similarity) / iters), stopped early.  Pins the
+ * prefixes of the long configs (C4, C5) whose full loops the oracle cannot finish quickly. */
+int klsh_oracle_cluster_prefix(klsh_oracle_state* st, float min_similarity, int iters,
+                               int run_iters, int bucket_size_threshold, klsh_oracle_rng* rng,
+                               uint64_t* nt_trace, int nthreads);
+
 /* p_cluster (reference function/cluster.cc:56-87) over the live rows taken as ONE bucket in
  * their current order; survivors become the live rows.  Returns the survivor count. */
 uint64_t klsh_oracle_pcluster(klsh_oracle_state* st, float threshold);

@@ -177,7 +177,11 @@ int main(int argc, char** argv) {
     const float min_sim = (float)atof(argv[argi]);
     const int iters = atoi(argv[argi + 1]);
     const int bthr = atoi(argv[argi + 2]);
-    Cluster(&v, min_sim, iters, 1, d, bthr, true);
+    // threads_to_use: 1 (T=1 semantics, deterministic) unless KLSH_REF_THREADS asks for more
+    // (timing only: at T>1 the reference's bucket order depends on scheduling, cluster.cc:281)
+    const char* te = getenv("KLSH_REF_THREADS");
+    const unsigned threads = te ? (unsigned)atoi(te) : 1u;
+    Cluster(&v, min_sim, iters, threads ? threads : 1u, d, bthr, true);
     save(&v, argv[argi + 3]);
     return 0;
   }
