@@ -197,64 +197,6 @@ __global__ __launch_bounds__(256) void k_scan_tile_sum(Src src, uint32_t n, uint
   if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
 }
 
-// One workgroup of 1024 lanes scans the tile sums in place (exclusive); *total = grand total.
-template <int kUnused = 0>
-__global__ __launch_bounds__(1024) void k_scan_tiles(uint32_t* tile_sums, uint32_t ntiles,
-                                                     uint32_t* total) {
-  __shared__ uint32_t wsum[17];
-  __shared__ uint32_t carry;
-  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (uint32_t c = 0; c < ntiles; c += 1024) {
-    const uint32_t i = c + threadIdx.x;
-    const uint32_t v = i < ntiles ? tile_sums[i] : 0u;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t a = 0;
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t t = wsum[k];
-        wsum[k] = a;
-        a += t;
-      }
-      wsum[16] = a;
-    }
-    __syncthreads();
-    if (i < ntiles) tile_sums[i] = carry + wsum[w] + x - v;
-    __syncthreads();
-    if (threadIdx.x == 0) carry += wsum[16];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *total = carry;
-}
-
-template <class Src, class Dst>
-__global__ __launch_bounds__(256) void k_scan_apply(Src src, Dst dst, uint32_t n,
-                                                    const uint32_t* __restrict__ tile_sums) {
-  const uint32_t base = blockIdx.x * (uint32_t)kScanTile + threadIdx.x * 16u;
-  uint32_t v[16];
-  uint32_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    v[k] = (base + k < n) ? src(base + k) : 0u;
-    acc += v[k];
-  }
-  uint32_t total;
-  uint32_t run = block_excl_scan_256(acc, &total) + tile_sums[blockIdx.x];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    if (base + k < n) dst(base + k, run, v[k]);
-    run += v[k];
-  }
-}
-
 // ------------------------------------------------------------ single-pass scan (look-back) ----
 // Tiles are taken in ticket order (atomic counter), so a tile only ever waits on tiles that are
 // already running.  Each tile publishes its aggregate at once, then its inclusive prefix once the
@@ -375,21 +317,6 @@ __global__ __launch_bounds__(256) void k_scan_lb(Src src, Dst dst, uint32_t n, u
   }
 }
 
-// Three-kernel variant (tile sums, one-workgroup scan of them, apply); KLSH_SCAN=3k selects it.
-template <class Src, class Dst>
-inline void device_scan_3k(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, uint32_t* total,
-                           hipStream_t s) {
-  const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
-  if (ntiles == 0) {
-    (void)hipMemsetAsync(total, 0, sizeof(uint32_t), s);
-    return;
-  }
-  uint32_t* ts = tile_sums + kScanSumsWord;  // apart from the look-back words
-  k_scan_tile_sum<Src><<<ntiles, 256, 0, s>>>(src, n, ts);
-  k_scan_tiles<0><<<1, 1024, 0, s>>>(ts, ntiles, total);
-  k_scan_apply<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, ts);
-}
-
 // Two-kernel variant: tile sums, then every tile sums the tile sums before it itself (ntiles^2/2
 // L2-resident reads in all: no single-workgroup scan, no waiting between workgroups).
 template <class Src, class Dst>
@@ -436,9 +363,6 @@ inline void device_scan_2k(Src src, Dst dst, uint32_t n, uint32_t* tile_sums, ui
   k_scan_apply_redundant<Src, Dst><<<ntiles, 256, 0, s>>>(src, dst, n, ts, total);
 }
 
-int scan_variant();  // KLSH_SCAN: 0 auto (default), 1 "2k", 2 "3k", 3 "lb" (look-back at any size)
-
-
 // Exclusive scan of src over [0, n) feeding dst(i, prefix, value); *total = sum.  `ws` is the
 // scan workspace (zeroed once at allocation, scan_ws_words(n) words).
 template <class Src, class Dst>
@@ -447,10 +371,7 @@ inline void device_scan(Src src, Dst dst, uint32_t n, uint32_t* ws, uint32_t* to
   // auto: the look-back kernel below 2^20 items (one launch; as fast as the others there), the
   // two-kernel scan above (tools/ubench_sort on MI355X: 18.5 vs 15.9 us at 1M, 201 vs 87 us at
   // 9.47M — look-back chains across ~2000 co-resident tiles)
-  int var = scan_variant();
-  if (var == 0 && n >= (1u << 20)) var = 1;
-  if (var == 1) return device_scan_2k(src, dst, n, ws, total, s);
-  if (var == 2) return device_scan_3k(src, dst, n, ws, total, s);
+  if (n >= (1u << 20)) return device_scan_2k(src, dst, n, ws, total, s);
   const uint32_t ntiles = (n + kScanTile - 1) / kScanTile;
   k_scan_lb<Src, Dst><<<ntiles ? ntiles : 1u, 256, 0, s>>>(src, dst, n, ws, total, err);
 }

@@ -147,7 +147,7 @@ struct klsh_ctx {
   uint64_t shard_cap = 0;
   double t_enqueued = 0.0;  // diagnostics (KLSH_ITER_LOG): host time when an iteration was queued
   // Counters through mapped pinned memory (klsh::Publish): the host polls pub_seq instead of a
-  // copy launch + stream sync after every iteration.  KLSH_ZERO_COPY=0: the copy + sync.
+  // copy launch + stream sync after every iteration (a copy + sync if mapped memory is refused).
   Counters* pub_host = nullptr;   // host view
   Counters* pub_dev = nullptr;    // device view of the same memory
   uint32_t* pub_seq_host = nullptr;
@@ -156,29 +156,13 @@ struct klsh_ctx {
   bool ctr_clean = false;  // *ctr is known to be zero (the publisher zeroed it)
   // Queued-ahead projection (small iterations, where no bucket can be oversize): the next
   // iteration's sign-hash is enqueued behind the compaction, reading N from n_next_dev, before
-  // the host has the counters.  KLSH_QUEUE_AHEAD=0: off.
+  // the host has the counters.
   uint32_t* n_next_dev = nullptr;
   bool spec_pending = false;
   uint64_t spec_k = 0;
   int spec_ev = 0;
-  bool queue_ahead = [] {
-    const char* e = getenv("KLSH_QUEUE_AHEAD");
-    return !(e && e[0] == '0');
-  }();
-  bool zero_copy = [] {
-    const char* e = getenv("KLSH_ZERO_COPY");
-    return !(e && e[0] == '0');
-  }();
-  // KLSH_GRID_HINTS=1: size the big-run grids from the previous iteration's run counts.  Off by
-  // default: measured slower on C2 (346 -> 370 ms; with fewer pending big-run workgroups the
-  // small-run waves take the CUs the big runs need).
-  // KLSH_GRID_HINTS: 1 = every big-run class, 2 = the two rarest (>384, >896 rows), 0 (default) =
-  // none.  Measured: all hints 346 -> 370 ms on C2; the rare-class hints neutral on C2/C5 but
-  // 3.42 -> 6.25 s on C4, whose >896-row runs are the critical path.
-  int grid_hints = [] {
-    const char* e = getenv("KLSH_GRID_HINTS");
-    return e ? atoi(e) : 0;
-  }();
+  bool zero_copy = true;
+  klsh::RunCounters* rc = nullptr;  // run-list counters (device, one 128-B line each)
 
   ~klsh_ctx() { release(); }
 
@@ -194,10 +178,7 @@ struct klsh_ctx {
   // (the late iterations are latency-bound on one GPU already), so every rank takes the whole
   // canonical order and runs the remaining iterations on its replica — identically, with no
   // communication.  klsh_set_option(ctx, "shard_min_rows", n); 0 = always sharded.
-  uint64_t shard_min_rows = [] {
-    const char* e = getenv("KLSH_SHARD_MIN_ROWS");
-    return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)(1u << 21);
-  }();
+  uint64_t shard_min_rows = 1u << 21;
 
   // "stop_after" (klsh_set_option): run only the first k iterations of a call's threshold
   // schedule (0 = all).  Prefix parity tests of the long configs use it; results of the
@@ -255,7 +236,7 @@ struct klsh_ctx {
   void release_state() {
     dfree(rows.x); dfree(rows.nrm); dfree(rows.cnt); dfree(rows.head); dfree(rows.tail);
     dfree(rows.nxt); dfree(order); dfree(alt); dfree(keys); dfree(keys2); dfree(nk1);
-    dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.seg); dfree(mw.over);
+    dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.over);
     dfree(mw.huge);
     dfree(pw.fix);
     dfree(pw.ws);
@@ -278,6 +259,8 @@ struct klsh_ctx {
     release_state();
     dfree(W);
     dfree(ctr);
+    dfree(rc);
+    mw.rc = nullptr;
     if (h_ctr) (void)hipHostFree(h_ctr);
     h_ctr = nullptr;
     dfree(n_next_dev);
@@ -321,7 +304,7 @@ struct klsh_ctx {
         (e = dalloc(&nv2, s)) ||
         (e = dalloc(&hist, klsh::sort_ws_words(s))) ||
         (e = dalloc(&tile_sums, klsh::scan_ws_words(s))) ||
-        (e = dalloc(&mw.seg, s + 64)) || (e = dalloc(&mw.over, s + 64)) ||
+        (e = dalloc(&mw.over, s + 64)) ||
         (e = dalloc(&pw.fix, s)) || (e = dalloc(&pw.ws, 64)) ||
         (e = dalloc(&mw.big[0], s / 65 + 64)) || (e = dalloc(&mw.big[1], s / 129 + 64)) ||
         (e = dalloc(&mw.big[2], s / 193 + 64)) || (e = dalloc(&mw.big[3], s / 385 + 64)) ||
@@ -388,6 +371,12 @@ struct klsh_ctx {
   }
   const float* hyperplane_ptr(uint64_t k) const { return W + (k - w_k0) * (uint64_t)dp; }
 
+  // zero the iteration counters (and the run-list counters) on the stream
+  int reset_counters() {
+    KLSH_HIP(hipMemsetAsync(ctr, 0, sizeof(Counters), stream));
+    KLSH_HIP(hipMemsetAsync(rc, 0, sizeof(klsh::RunCounters), stream));
+    return 0;
+  }
   int sync_counters() {
     ctr_clean = false;
     KLSH_HIP(hipMemcpyAsync(h_ctr, ctr, sizeof(Counters), hipMemcpyDeviceToHost, stream));
@@ -476,8 +465,7 @@ klsh_ctx* klsh_create(int device, int* err) {
   // path, a normal-priority main stream doubled their time (KLSH_BIG_PRIORITY=0: all equal)
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  const char* bp = getenv("KLSH_BIG_PRIORITY");
-  const bool big_prio = !(bp && bp[0] == '0');
+  const bool big_prio = true;
   bool ok = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking,
                                         big_prio ? prio_hi : prio_lo) == hipSuccess;
   for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
@@ -490,6 +478,9 @@ klsh_ctx* klsh_create(int device, int* err) {
   ok = ok && hipMalloc((void**)&c->ctr, sizeof(Counters)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) == hipSuccess;
   ok = ok && hipMemset(c->ctr, 0, sizeof(Counters)) == hipSuccess;  // err starts clear
+  ok = ok && hipMalloc((void**)&c->rc, sizeof(klsh::RunCounters)) == hipSuccess &&
+       hipMemset(c->rc, 0, sizeof(klsh::RunCounters)) == hipSuccess;
+  c->mw.rc = c->rc;
   ok = ok && hipMalloc((void**)&c->n_next_dev, 64) == hipSuccess &&
        hipMemset(c->n_next_dev, 0, 64) == hipSuccess;
   if (ok && c->zero_copy) {
@@ -609,7 +600,7 @@ int klsh_load_counts(klsh_ctx* ctx, const uint16_t* counts, uint64_t n_total,
       rc = fail(KLSH_E_HIP, "lut upload");
       break;
     }
-    if (hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s) != hipSuccess) {
+    if (ctx->reset_counters()) {
       rc = fail(KLSH_E_HIP, "counter reset");
       break;
     }
@@ -695,7 +686,7 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[3], s));
   const bool zc = sync && ctx->zero_copy;
   klsh::Publish pub{ctx->pub_dev, ctx->pub_seq_dev, ++ctx->pub_seq, ctx->n_next_dev};
-  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s, zc ? &pub : nullptr);
+  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s, zc ? &pub : nullptr, ctx->rc);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
   if (zc && after)  // work queued behind the compaction before the host waits for it
@@ -753,17 +744,15 @@ static int merge_nested(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, f
     klsh::launch_project(ctx->rows, fv + p, ctx->nk1, b, ctx->hyperplane_ptr(k), h2, key_or, s,
                          &ctx->pw);
     uint32_t *rk = nullptr, *rv = nullptr;
-    klsh::radix_sort(ctx->nk1, fv + p, ctx->nk2, ctx->nv2, b, h2, ctx->hist, ctx->tile_sums,
-                     ctx->ctr, &rk, &rv, s);
+    klsh::radix_sort(ctx->nk1, fv + p, ctx->nk2, ctx->nv2, b, h2, ctx->hist, &rk, &rv, s);
     KLSH_HIP(hipMemcpyAsync(fk + p, rk, 4ull * b, hipMemcpyDeviceToDevice, s));
     if (rv != fv + p) KLSH_HIP(hipMemcpyAsync(fv + p, rv, 4ull * b, hipMemcpyDeviceToDevice, s));
-    // fresh run lists for the region (n_seg .. n_over are contiguous)
-    KLSH_HIP(hipMemsetAsync(&ctx->ctr->n_seg, 0,
-                            offsetof(Counters, total) - offsetof(Counters, n_seg), s));
+    // fresh run lists for the region
+    KLSH_HIP(hipMemsetAsync(ctx->rc, 0, sizeof(klsh::RunCounters), s));
     klsh::launch_merge(ctx->rows, fk, fv, p, p + b, thr, -1, ctx->mw, ctx->ctr, s);
     KLSH_HIP(hipGetLastError());
   }
-  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s);
+  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s, nullptr, ctx->rc);
   KLSH_HIP(hipGetLastError());
   return ctx->sync_counters();
 }
@@ -777,38 +766,14 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
                              const std::function<int(uint32_t*)>* after = nullptr) {
   uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
   if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, st, timed, true, after)) return e;
-  // the next iteration's big-run grids: twice this iteration's run counts (plus slack)
-  uint32_t next_hint[klsh::kBigClasses + 1];
-  for (int c = 0; c < klsh::kBigClasses; ++c) next_hint[c] = 2 * ctx->h_ctr->n_big[c] + 4;
-  next_hint[klsh::kBigClasses] = 2 * ctx->h_ctr->n_huge + 2;
-  uint32_t small_batches = (ctx->h_ctr->n_cls[0] + 63) / 64;
-  for (int c = 1; c < klsh::kGroupClasses; ++c) {
-    const uint32_t per = 64u >> (c + 1);  // runs per batch: 64 / G, G = 2 << c
-    small_batches += (ctx->h_ctr->n_cls[c] + per - 1) / per;
-  }
-  const uint32_t next_small = std::max<uint32_t>(2 * small_batches + 64, 256);
-  static const uint32_t big896_aux_min = [] {  // KLSH_BIG896_AUX_MIN: runs that move the class
-    const char* e = getenv("KLSH_BIG896_AUX_MIN");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : 64u;
-  }();
-  ctx->mw.big896_aux = ctx->h_ctr->n_big[klsh::kBigClasses - 1] >= big896_aux_min ? 1u : 0u;
+  // many 385..896-row runs this iteration: the next one runs that class on an auxiliary stream
+  ctx->mw.big896_aux = ctx->h_ctr->n_big[klsh::kBigClasses - 1] >= 64u ? 1u : 0u;
   if (ctx->h_ctr->n_over > 0) {
     std::vector<uint2> over;
     uint64_t hyp = 0;
     if (int e = oversize_runs(ctx, &over, &hyp)) return e;
-    memset(ctx->mw.hint, 0, sizeof(ctx->mw.hint));  // nested regions: no history
-    ctx->mw.hint_small = 0;
     if (int e = merge_nested(ctx, fk, fv, n, thr, over, seed_base, rng_counter, out, st))
       return e;
-  }
-  if (ctx->grid_hints == 1) {
-    memcpy(ctx->mw.hint, next_hint, sizeof(next_hint));
-    ctx->mw.hint_small = next_small;
-  } else if (ctx->grid_hints == 2) {
-    // the two rarest, most LDS-hungry classes (>384 rows: 142 KB, >896 rows: 64+ KB per
-    // workgroup) only
-    ctx->mw.hint[klsh::kBigClasses - 1] = next_hint[klsh::kBigClasses - 1];
-    ctx->mw.hint[klsh::kBigClasses] = next_hint[klsh::kBigClasses];
   }
   if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
   ctx->n_live = ctx->h_ctr->total;
@@ -846,7 +811,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     if (queued && ctx->spec_k != k) return fail(KLSH_E_STATE, "queued projection out of step");
     const int e0 = queued ? ctx->spec_ev : 0;
     if (!queued) {
-      if (!ctx->ctr_clean) KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+      if (!ctx->ctr_clean) if (int e = ctx->reset_counters()) return e;
       KLSH_HIP(hipEventRecord(ctx->ev[e0], s));
       klsh::launch_project(ctx->rows, ctx->order, ctx->keys, (uint32_t)n, ctx->hyperplane_ptr(k), h,
                            0u, s, &ctx->pw);
@@ -856,7 +821,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     ctx->ctr_clean = false;
     uint32_t *fk = nullptr, *fv = nullptr;
     klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n, h, ctx->hist,
-                     ctx->tile_sums, ctx->ctr, &fk, &fv, s);
+                     &fk, &fv, s);
     KLSH_HIP(hipGetLastError());
     if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[5], s));
     if (const char* path = getenv("KLSH_BUCKET_STATS")) {  // diagnostics: run-length histogram
@@ -890,7 +855,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     // to have oversize buckets (nestedCluster changes rows and draws hyperplanes first), the
     // queued keys are simply recomputed; they go to ctx->keys, which the nested work must not be
     // reading — so only when the sorted keys of this iteration are in the other buffer.
-    const bool ahead = ctx->queue_ahead && ctx->zero_copy && it + 1 < it_end &&
+    const bool ahead = ctx->zero_copy && it + 1 < it_end &&
                        klsh::project_device_n_ok(ctx->d) && !getenv("KLSH_BUCKET_STATS") &&
                        (fk != ctx->keys || (bucket_size_threshold >= 0 &&
                                             n <= (uint64_t)bucket_size_threshold));
@@ -1022,7 +987,7 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations, 
     if (int e = ctx->ensure_hyperplanes(seed_base, k, (uint64_t)h, &st->host_ms)) return e;
 
     // 1. keys of my rows, key-range ownership, send counts
-    if (!ctx->ctr_clean) KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+    if (!ctx->ctr_clean) if (int e = ctx->reset_counters()) return e;
     ctx->ctr_clean = false;
     KLSH_HIP(hipEventRecord(ctx->ev[0], s));
     klsh::launch_project(ctx->rows, ctx->order, ctx->keys, n_g, ctx->hyperplane_ptr(k), h, 0u, s,
@@ -1062,8 +1027,7 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations, 
 
     // 3. bucket order of my key range, merge, compaction, delta list
     uint32_t *fk = nullptr, *fv = nullptr;
-    klsh::radix_sort(ctx->keys, ctx->alt, ctx->keys2, ctx->order, m_g, h, ctx->hist,
-                     ctx->tile_sums, ctx->ctr, &fk, &fv, s);
+    klsh::radix_sort(ctx->keys, ctx->alt, ctx->keys2, ctx->order, m_g, h, ctx->hist, &fk, &fv, s);
     KLSH_HIP(hipGetLastError());
     if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[5], s));
     uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
@@ -1209,10 +1173,8 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   const float sim_step = (max_similarity - min_similarity) / (float)iterations;
   float threshold = max_similarity;
 
-  memset(ctx->mw.hint, 0, sizeof(ctx->mw.hint));  // no run counts seen yet in this call
   ctx->ctr_clean = false;
   ctx->spec_pending = false;
-  ctx->mw.hint_small = 0;
   // no run counts yet: only very large inputs start with the 385..896-row class on aux 2
   ctx->mw.big896_aux = ctx->n_live >= (1u << 24) ? 1u : 0u;
   // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
@@ -1436,7 +1398,7 @@ int klsh_bucket_sort(klsh_ctx* ctx, const uint32_t* keys, uint64_t n, int bits,
       hipMemcpyAsync(v0, iota.data(), 4 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
     rc = fail(KLSH_E_HIP, "upload");
   } else {
-    klsh::radix_sort(k0, v0, k1, v1, (uint32_t)n, bits, ws, ts, ctr, &ok, &ov, s);
+    klsh::radix_sort(k0, v0, k1, v1, (uint32_t)n, bits, ws, &ok, &ov, s);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(sorted_keys, ok, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(perm, ov, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1458,7 +1420,7 @@ int klsh_pcluster(klsh_ctx* ctx, float thr) {
   const uint32_t n = (uint32_t)ctx->n_live;
   if (n == 0) return 0;
   hipStream_t s = ctx->stream;
-  KLSH_HIP(hipMemsetAsync(ctx->ctr, 0, sizeof(Counters), s));
+  if (int e = ctx->reset_counters()) return e;
   KLSH_HIP(hipMemsetAsync(ctx->keys, 0, 4ull * n, s));  // one bucket: every key equal
   uint64_t dummy = 0;
   if (int e = merge_and_compact(ctx, ctx->keys, ctx->order, n, thr, -1, 0, &dummy, nullptr, false))

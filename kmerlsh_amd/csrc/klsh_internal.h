@@ -11,16 +11,10 @@ namespace klsh {
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;  // dead position marker in a bucket's slot run
 constexpr uint32_t kNil = 0xFFFFFFFFu;      // end of a member list
 constexpr int kMaxHyperplanes = 32;         // keys are uint32 (h = floor(log2 N) <= 31)
-constexpr int kRadixTile = 2048;            // keys per radix-sort workgroup (256 lanes x 8 rounds)
 constexpr int kScanTile = 4096;             // items per scan workgroup (256 lanes x 16)
-constexpr uint32_t kSortStatusWord = 2048;  // sort workspace: small words, then tile status
-// Sort workspace words for `slots` keys (onesweep: 256 u64 status words per tile) and scan
-// workspace words (64 small words + one u64 status word per scan tile; at least what the
-// three-kernel scan variant needs).  Both are zeroed once at allocation.
-inline uint64_t sort_ws_words(uint64_t slots) {
-  // onesweep status (256 u64 per tile) or an LSD [digit][tile] histogram of up to 1024 digits
-  return kSortStatusWord + 1024ull * ((slots + kRadixTile - 1) / kRadixTile) + 256;
-}
+// Sort workspace (u32 words) for `slots` keys: [digit][tile] counts and digit totals
+// (klsh_sort.hip).
+uint64_t sort_ws_words(uint64_t slots);
 // Scan workspace (u32 words): [0, 64) ticket / done / epoch of the look-back scan, then its 64-bit
 // tile status words (room for 2^32 items), then the tile sums of the multi-kernel scans and of
 // the compaction — apart, so a tile sum can never pass for a look-back status word.
@@ -43,9 +37,21 @@ constexpr int kBigRows[kBigClasses] = {128, 192, 384, 896};
 constexpr int kGroupClasses = 6;
 inline uint64_t group_class_capacity(int c, uint64_t cap) { return cap / ((1ull << c) + 1) + 64; }
 
+// Run-list counters: k_runs' workgroups add to each of them once, so each sits on a 128-B line of
+// its own (adds to one line serialise at ~5-10 ns each; 13 counters on one line made k_runs
+// ~10x slower than its key reads).  Device only: the compaction copies them into Counters for
+// the host and zeroes them for the next iteration.
+struct alignas(128) CountLine {
+  uint32_t v;
+  uint32_t pad_[31];
+};
+struct RunCounters {
+  CountLine n_seg, n_cls[kGroupClasses], n_big[kBigClasses], n_huge, n_over;
+};
+
 // Device-side per-iteration counters (zeroed by the host before each iteration).
 struct Counters {
-  uint32_t n_seg;                  // bucket runs found by the segment scan
+  uint32_t n_seg;                  // bucket runs (k_runs)
   uint32_t n_cls[kGroupClasses];   // runs of 2..64 rows queued per size class
   uint32_t n_big[kBigClasses];     // runs of 65..896 rows queued for k_merge_big, per class
   uint32_t n_huge;                 // longer runs queued for k_merge_huge
@@ -58,12 +64,12 @@ struct Counters {
 
 // Merge workspace (device), sized for `cap` positions.
 struct MergeWork {
-  uint32_t* seg;                   // run starts [n_seg]
   uint2* cls[kGroupClasses];       // (start, length) of runs per size class
   uint2* big[kBigClasses];         // (start, length) of runs for k_merge_big, per class
   uint2* huge;                     // (start, length) of runs for k_merge_huge
   uint2* over;                     // (start, length) of oversize runs
   uint32_t* tile_sums;
+  RunCounters* rc;                 // the run counts of this iteration (device)
   // Sharded loop only (nullptr otherwise): every survivor a merge rewrote is appended to dlist
   // (ctr->n_delta entries, any order, each slot once); mark[slot] == stamp dedupes the kernels
   // that merge in place (stamp: unique per iteration, never reused by a context).
@@ -73,12 +79,6 @@ struct MergeWork {
   // Size classes run concurrently on kMergeStreams auxiliary streams (fork after the run
   // classification, join before the compaction): in the late, small iterations each class kernel
   // is one long sequential walk, and serialised walks would add up.  aux[0] == nullptr: one stream.
-  // Grid hints for the big-run / huge-run kernels (0 = none: size for the worst case).  Their
-  // workgroups need most of a CU's LDS, so even empty ones wait for a free CU; the engine passes
-  // twice the previous iteration's run counts (the kernels loop over their lists, so any grid
-  // is correct).
-  uint32_t hint[kBigClasses + 1];
-  uint32_t hint_small;  // the same for the fused small-run kernel (batches)
   // 385..896-row runs on aux 2 instead of ahead of the >896-row runs on the main stream: set by
   // the engine when the previous iteration had many of them (C4: thousands; C2: < 10)
   uint32_t big896_aux;
@@ -145,11 +145,10 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
                     const float* W, int h, uint32_t key_or, hipStream_t s,
                     const ProjectWork* pw = nullptr);
 
-// Stable LSD radix sort of (keys, vals)[0..n) on the low `bits` bits. Uses ping-pong buffers;
-// returns via *out_k/*out_v which pair holds the result (one of (k0,v0) or (k1,v1)).
+// Stable LSD radix sort of (keys, vals)[0..n) on the low `bits` bits (klsh_sort.hip); ping-pong
+// buffers, *out_k/*out_v = the pair holding the result.  ws: sort_ws_words(n) words.
 void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
-                uint32_t* hist, uint32_t* tile_sums, Counters* ctr, uint32_t** out_k,
-                uint32_t** out_v, hipStream_t s);
+                uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s);
 
 // Greedy merge (p_cluster) over every bucket run of equal key in positions [lo, hi) of
 // (key, slots), in place: survivors first in each run, kInvalid after.  Runs longer than
@@ -167,9 +166,11 @@ struct Publish {
   uint32_t* n_next;   // device word that also receives the survivor count (may be null)
 };
 
-// out[0..total) = slots[p] for p with slots[p] != kInvalid, stable; ctr->total = count.
+// out[0..total) = slots[p] for p with slots[p] != kInvalid, stable; ctr->total = count.  rc (may
+// be null): the iteration's run counters, copied into *ctr (and zeroed) before the publish.
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
-                    Counters* ctr, hipStream_t s, const Publish* pub = nullptr);
+                    Counters* ctr, hipStream_t s, const Publish* pub = nullptr,
+                    RunCounters* rc = nullptr);
 
 // Mode-C producer: rows x[i] (slot i) from counts (d x bs, sample-major), LUT ln(c+1),
 // v_kmers; order[] = kept rows (sum > 0.1 d) compacted; ctr->total = kept count.

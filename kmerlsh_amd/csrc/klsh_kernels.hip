@@ -25,58 +25,6 @@
 namespace klsh {
 
 // ========================================================================= projection ==========
-// One lane per live row; the row sits in registers, the h hyperplanes in LDS (broadcast reads).
-// STAGED: rows are gathered coalesced through a per-wave LDS tile (stage_rows); otherwise each
-// lane loads its own row.  Four hyperplanes are summed at once (four independent chains); the
-// order inside each is the reference's: s = ((0 + w0 x0) + w1 x1) + ...
-template <int D, bool STAGED>
-__global__ __launch_bounds__(256) void k_project(const float* __restrict__ X, int dp,
-                                                 const uint32_t* __restrict__ slots,
-                                                 uint32_t* __restrict__ keys, uint32_t n,
-                                                 const float* __restrict__ W, int h,
-                                                 uint32_t key_or) {
-  __shared__ __attribute__((aligned(16))) float sw[kMaxHyperplanes * D];
-  __shared__ __attribute__((aligned(16))) float tile[STAGED ? 4 : 1][STAGED ? 64 * (D + 4) : 4];
-  for (int i = threadIdx.x; i < h * D; i += 256) sw[i] = W[(i / D) * dp + (i % D)];
-  const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-  const bool valid = p < n;
-  float x[D];
-  if constexpr (STAGED) {
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    stage_rows<D>(X, dp, valid ? slots[p] : 0u, valid, tile[wv]);
-    __syncthreads();
-    if (!valid) return;
-    load_row<D>(tile[wv] + lane * (D + 4), x);
-  } else {
-    __syncthreads();
-    if (!valid) return;
-    load_row<D>(X + (size_t)slots[p] * dp, x);
-  }
-  uint32_t key = 0;
-  int j = 0;
-  for (; j + 4 <= h; j += 4) {
-    const float* w0 = sw + j * D;
-    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      s0 = s0 + w0[k] * x[k];
-      s1 = s1 + w0[D + k] * x[k];
-      s2 = s2 + w0[2 * D + k] * x[k];
-      s3 = s3 + w0[3 * D + k] * x[k];
-    }
-    key = key * 16u + (s0 >= 0.0f ? 8u : 0u) + (s1 >= 0.0f ? 4u : 0u) + (s2 >= 0.0f ? 2u : 0u) +
-          (s3 >= 0.0f ? 1u : 0u);
-  }
-  for (; j < h; ++j) {
-    const float* w = sw + j * D;
-    float s = 0.0f;
-#pragma unroll
-    for (int k = 0; k < D; ++k) s = s + w[k] * x[k];
-    key = key * 2u + (s >= 0.0f ? 1u : 0u);
-  }
-  keys[p] = key | key_or;
-}
-
 // Packed-f32 projection.  The same sequential chains as k_project, two per instruction:
 // v_pk_mul_f32 / v_pk_add_f32 round each half exactly like v_mul_f32 / v_add_f32 (no fusion,
 // -ffp-contract=off), so the keys are bit-identical, at twice the f32 VALU issue rate — the
@@ -658,25 +606,24 @@ void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* key
   }
 }
 
+// The projection of a call: d in {8, 16, 32, 64} the packed VALU kernel (or, with
+// KLSH_PROJECT=mfma, the certified matrix-core kernel, bit-exact but measured slower at d <= 64:
+// 161-167 vs 140-145 us per C2 launch — its per-pair bound test and ballots cost what the packed
+// chains cost); wider rows the certified matrix-core screen + exact fix-up pass (pw given), else
+// the packed wide-row kernel (hyperplanes in LDS), else the generic kernel.
+static bool project_mfma_requested() {
+  static const bool v = [] {
+    const char* e = getenv("KLSH_PROJECT");
+    return e && std::string(e) == "mfma";
+  }();
+  return v;
+}
+
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
                     const float* W, int h, uint32_t key_or, hipStream_t s, const ProjectWork* pw) {
   if (n == 0) return;
   const dim3 grid((n + 255) / 256), block(256);
-  // KLSH_PROJECT: "pk2" (default: packed f32, 8 chains, 1 row per lane) | "mfma" (matrix cores,
-  // d in {16, 32, 64}) | "pk2r" (2 rows per
-  // lane; 4 for wide rows) | "pk" (4 chains) | "scalar" | "staged".  Measured on C2/C5: the extra
-  // rows per lane only add register pressure (the kernel is not LDS-read bound).
-  static const int variant = [] {
-    const char* e = getenv("KLSH_PROJECT");
-    if (!e) return 1;
-    const std::string v(e);
-    return v == "pk" ? 0 : v == "pk2r" ? 4 : v == "scalar" ? 2 : v == "staged" ? 3 : v == "pk2" ? 5 : v == "mfma" ? 6 : 1;
-  }();
-  const bool staged = variant == 3;
-  const dim3 grid2((n + 511) / 512);
-  // wide rows: the matrix-core kernel + exact fix-ups (default when the workspace is given;
-  // KLSH_PROJECT=pk2 keeps the packed VALU kernel)
-  if (pw && r.d > 64 && h > 0 && (variant == 1 || variant == 6)) {
+  if (pw && r.d > 64 && h > 0) {
     const size_t lds = (size_t)((r.d + 15) / 16) * 64 * 2 * 16 + 32 * sizeof(float);
     const size_t flds = sizeof(float) * (size_t)h * r.dp;  // the fix-up kernel's hyperplanes
     if (lds <= 96 * 1024 && flds <= 128 * 1024) {
@@ -694,16 +641,9 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
       return;
     }
   }
-  // the certified matrix-core kernel (KLSH_PROJECT=mfma): bit-exact, but at d <= 64 its
-  // per-pair epilogue (bound test + ballots) costs about what the packed chains cost — measured
-  // 161-167 vs 140-145 us per C2 launch — so the packed VALU kernel stays the default
-  if (variant == 6 && (r.d == 16 || r.d == 32 || r.d == 64)) {
+  if (project_mfma_requested() && (r.d == 16 || r.d == 32 || r.d == 64)) {
     const uint32_t groups = (n + 127) / 128;  // 4 waves x 32 rows per workgroup per step
-    static const uint32_t cap = [] {  // KLSH_PROJECT_GRID: persistent grid cap (A/B)
-      const char* e = getenv("KLSH_PROJECT_GRID");
-      return e ? (uint32_t)atoi(e) : 8192u;
-    }();
-    const dim3 gm(std::min<uint32_t>(groups, cap));
+    const dim3 gm(std::min<uint32_t>(groups, 8192u));
     const float eps = project_eps(r.d);
     if (r.d == 64) k_project_mfma<64><<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
     else if (r.d == 32) k_project_mfma<32><<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
@@ -711,42 +651,18 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
     return;
   }
   switch (r.d) {
-#define KLSH_PROJECT_CASE(DD)                                                                     \
-  case DD:                                                                                      \
-    if (variant == 4)                                                                           \
-      k_project_pk<DD, 2, 2><<<grid2, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);  \
-    else if (variant == 0)                                                                      \
-      k_project_pk<DD, 1, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);   \
-    else if (variant == 1 || variant == 5)                                                      \
-      k_project_pk<DD, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);   \
-    else if (staged)                                                                            \
-      k_project<DD, true><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);      \
-    else                                                                                        \
-      k_project<DD, false><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or);     \
-    break;
-    KLSH_PROJECT_CASE(8)
-    KLSH_PROJECT_CASE(16)
-    KLSH_PROJECT_CASE(32)
-    KLSH_PROJECT_CASE(64)
-#undef KLSH_PROJECT_CASE
+    case 8: k_project_pk<8, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
+    case 16: k_project_pk<16, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
+    case 32: k_project_pk<32, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
+    case 64: k_project_pk<64, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
     default: {
       const size_t lds = sizeof(float4) * (size_t)r.dp * (size_t)((h + 3) / 4);
-      if (variant != 2 && lds <= 64 * 1024) {
-        static const bool lds_ok = [] {
-          bool ok = true;
-          for (const void* f : {reinterpret_cast<const void*>(&k_project_wide_pk<1>),
-                                reinterpret_cast<const void*>(&k_project_wide_pk<4>)})
-            ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           64 * 1024) == hipSuccess;
-          return ok;
-        }();
+      if (lds <= 64 * 1024) {
+        static const bool lds_ok =
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_wide_pk<1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;
         (void)lds_ok;
-        if (variant == 4)
-          k_project_wide_pk<4><<<(n + 1023) / 1024, block, lds, s>>>(r.x, r.d, r.dp, slots, keys,
-                                                                     n, W, h, key_or);
-        else
-          k_project_wide_pk<1><<<grid, block, lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h,
-                                                        key_or);
+        k_project_wide_pk<1><<<grid, block, lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or);
       } else {
         k_project_generic<<<grid, block, 0, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or);
       }
@@ -776,6 +692,27 @@ __global__ __launch_bounds__(256) void k_compact_count(const uint32_t* __restric
   if (t == 0) counts[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
+// The iteration's run counts (k_runs, k_merge_huge's list) into *ctr, and rc back to zero.
+__device__ __forceinline__ void collect_run_counts(Counters* ctr, RunCounters* rc) {
+  if (!rc) return;
+  ctr->n_seg = rc->n_seg.v;
+  rc->n_seg.v = 0u;
+#pragma unroll
+  for (int c = 0; c < kGroupClasses; ++c) {
+    ctr->n_cls[c] = rc->n_cls[c].v;
+    rc->n_cls[c].v = 0u;
+  }
+#pragma unroll
+  for (int c = 0; c < kBigClasses; ++c) {
+    ctr->n_big[c] = rc->n_big[c].v;
+    rc->n_big[c].v = 0u;
+  }
+  ctr->n_huge = rc->n_huge.v;
+  rc->n_huge.v = 0u;
+  ctr->n_over = rc->n_over.v;
+  rc->n_over.v = 0u;
+}
+
 // Publish the iteration's counters to the host (see Publish), `total` filled in.
 __device__ __forceinline__ void publish_counters(Counters* ctr, uint32_t total, const Publish& pub) {
   Counters c = *ctr;
@@ -791,14 +728,18 @@ __device__ __forceinline__ void publish_counters(Counters* ctr, uint32_t total, 
   __hip_atomic_store(pub.seq_host, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void k_publish(Counters* ctr, Publish pub) { publish_counters(ctr, ctr->total, pub); }
+__global__ void k_publish(Counters* ctr, Publish pub, RunCounters* rc) {
+  collect_run_counts(ctr, rc);
+  if (pub.host) publish_counters(ctr, ctr->total, pub);
+}
 
 __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restrict__ slots,
                                                        uint32_t n,
                                                        const uint32_t* __restrict__ counts,
                                                        uint32_t* __restrict__ out,
                                                        uint32_t* __restrict__ total,
-                                                       Counters* ctr, Publish pub) {
+                                                       Counters* ctr, Publish pub,
+                                                       RunCounters* rc) {
   constexpr int K = kCompactTile / 256;
   __shared__ uint32_t cnt[K * 4], pre[K * 4 + 1], wsum[4];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -834,498 +775,24 @@ __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restric
     if (v[k] != kInvalid) out[pre[k * 4 + wv] + (uint32_t)__popcll(m[k] & below)] = v[k];
   if (blockIdx.x == gridDim.x - 1 && t == 0) {
     *total = pre[K * 4];
+    collect_run_counts(ctr, rc);
     if (pub.host) publish_counters(ctr, pre[K * 4], pub);
   }
 }
 
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
-                    Counters* ctr, hipStream_t s, const Publish* pub) {
-  if (scan_variant() == 2 || n == 0) {  // KLSH_SCAN=3k: the generic scan (A/B)
-    device_scan(SrcLive{slots}, DstCompact{slots, out}, n, tile_sums, &ctr->total, &ctr->err, s);
-    if (pub) k_publish<<<1, 1, 0, s>>>(ctr, *pub);  // after the scan: total is final
+                    Counters* ctr, hipStream_t s, const Publish* pub, RunCounters* rc) {
+  const Publish none{nullptr, nullptr, 0u, nullptr};
+  if (n == 0) {
+    (void)hipMemsetAsync(&ctr->total, 0, sizeof(uint32_t), s);
+    k_publish<<<1, 1, 0, s>>>(ctr, pub ? *pub : none, rc);
     return;
   }
   const uint32_t ntiles = (n + kCompactTile - 1) / kCompactTile;
   uint32_t* counts = tile_sums + kScanSumsWord;
   k_compact_count<<<ntiles, 256, 0, s>>>(slots, n, counts);
-  k_compact_apply<<<ntiles, 256, 0, s>>>(slots, n, counts, out, &ctr->total, ctr,
-                                         pub ? *pub : Publish{nullptr, nullptr, 0u, nullptr});
-}
-
-// ========================================================================== radix sort ==========
-// Stable LSD radix sort, 8-bit digits.  hist layout [digit][tile] so that one exclusive scan of
-// the flattened array gives every (digit, tile) its global output offset.
-__global__ __launch_bounds__(256) void k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n,
-                                                    int shift, uint32_t ntiles,
-                                                    uint32_t* __restrict__ hist) {
-  __shared__ uint32_t c[256];
-  c[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t base = blockIdx.x * (uint32_t)kRadixTile;
-  for (int r = 0; r < kRadixTile / 256; ++r) {
-    const uint32_t i = base + r * 256u + threadIdx.x;
-    if (i < n) atomicAdd(&c[(keys[i] >> shift) & 255u], 1u);
-  }
-  __syncthreads();
-  hist[threadIdx.x * ntiles + blockIdx.x] = c[threadIdx.x];
-}
-
-// Each tile is processed in 8 rounds of 256 keys in input order; inside a round the rank of a
-// key among equal digits is (earlier waves' counts) + (lower lanes' count from a 64-lane match
-// mask built with 8 ballots), so the scatter is stable.
-__global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ kin,
-                                                       const uint32_t* __restrict__ vin,
-                                                       uint32_t* __restrict__ kout,
-                                                       uint32_t* __restrict__ vout, uint32_t n,
-                                                       int shift, uint32_t ntiles,
-                                                       const uint32_t* __restrict__ hist) {
-  __shared__ uint32_t base[256];
-  __shared__ uint32_t wcnt[4][256];
-  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  base[t] = hist[t * ntiles + blockIdx.x];
-  wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
-  __syncthreads();
-  const uint32_t tile0 = blockIdx.x * (uint32_t)kRadixTile;
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int r = 0; r < kRadixTile / 256; ++r) {
-    const uint32_t i = tile0 + r * 256u + t;
-    const bool valid = i < n;
-    const uint32_t k = valid ? kin[i] : 0u;
-    const uint32_t v = valid ? vin[i] : 0u;
-    const uint32_t dig = (k >> shift) & 255u;
-    uint64_t match = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const bool bit = (dig >> b) & 1u;
-      const uint64_t m = __ballot(bit);
-      match &= bit ? m : ~m;
-    }
-    const uint32_t rank = __popcll(match & lt_mask);
-    if (valid && rank == 0) wcnt[w][dig] = __popcll(match);
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = base[dig] + rank;
-      for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dig];
-      kout[pos] = k;
-      vout[pos] = v;
-    }
-    __syncthreads();
-    base[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
-    __syncthreads();
-  }
-}
-
-// The same stable scatter, staged: the tile is first ordered by digit in LDS (positions from the
-// tile's own digit counts, ranks as in k_radix_scatter), then written out by consecutive lanes —
-// each digit's keys of the tile land in one contiguous run of the output instead of 2048
-// scattered 4-byte writes.
-__global__ __launch_bounds__(256) void k_radix_scatter_lds(const uint32_t* __restrict__ kin,
-                                                           const uint32_t* __restrict__ vin,
-                                                           uint32_t* __restrict__ kout,
-                                                           uint32_t* __restrict__ vout, uint32_t n,
-                                                           int shift, uint32_t ntiles,
-                                                           const uint32_t* __restrict__ hist) {
-  __shared__ uint32_t lk[kRadixTile], lv[kRadixTile];
-  __shared__ uint32_t gbase[256];   // global offset of the tile's first key of each digit
-  __shared__ uint32_t lstart[256];  // tile-local offset of each digit
-  __shared__ uint32_t run[256];     // keys of each digit placed so far
-  __shared__ uint32_t wcnt[4][256];
-  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  const uint32_t tile0 = blockIdx.x * (uint32_t)kRadixTile;
-  const uint32_t m = min((uint32_t)kRadixTile, n - tile0);
-  // global offsets of the tile's digits (the scanned [digit][tile] histogram)
-  gbase[t] = hist[t * ntiles + blockIdx.x];
-  run[t] = 0;
-  wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
-  __syncthreads();
-  // local digit counts: atomics in LDS
-  for (uint32_t i = t; i < m; i += 256) atomicAdd(&wcnt[0][(kin[tile0 + i] >> shift) & 255u], 1u);
-  __syncthreads();
-  {
-    uint32_t total;
-    lstart[t] = block_excl_scan_256(wcnt[0][t], &total);
-  }
-  wcnt[0][t] = 0;
-  __syncthreads();
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int r = 0; r < kRadixTile / 256; ++r) {
-    const uint32_t i = r * 256u + t;
-    const bool valid = i < m;
-    const uint32_t k = valid ? kin[tile0 + i] : 0u;
-    const uint32_t v = valid ? vin[tile0 + i] : 0u;
-    const uint32_t dig = (k >> shift) & 255u;
-    uint64_t match = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const bool bit = (dig >> b) & 1u;
-      const uint64_t mb = __ballot(bit);
-      match &= bit ? mb : ~mb;
-    }
-    const uint32_t rank = __popcll(match & lt_mask);
-    if (valid && rank == 0) wcnt[w][dig] = __popcll(match);
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = lstart[dig] + run[dig] + rank;
-      for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dig];
-      lk[pos] = k;
-      lv[pos] = v;
-    }
-    __syncthreads();
-    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
-    __syncthreads();
-  }
-  // write out in LDS order: entry e of digit d goes to gbase[d] + (e - lstart[d])
-  for (uint32_t e = t; e < m; e += 256) {
-    const uint32_t k = lk[e];
-    const uint32_t d = (k >> shift) & 255u;
-    const uint32_t pos = gbase[d] + (e - lstart[d]);
-    kout[pos] = k;
-    vout[pos] = lv[e];
-  }
-}
-
-// ------------------------------------------------------------- wider digits (small sorts) -----
-// The same two kernels for a B-bit digit (B = 9 or 10), so a key of up to 2B bits sorts in two
-// passes instead of three: the small late iterations (h <= 20) pay per launch, not per byte.
-template <int B>
-__global__ __launch_bounds__(256) void k_radix_hist_w(const uint32_t* __restrict__ keys, uint32_t n,
-                                                      int shift, uint32_t ntiles,
-                                                      uint32_t* __restrict__ hist) {
-  constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u;
-  __shared__ uint32_t c[RAD];
-  for (uint32_t d = threadIdx.x; d < RAD; d += 256) c[d] = 0;
-  __syncthreads();
-  const uint32_t base = blockIdx.x * (uint32_t)kRadixTile;
-  for (int r = 0; r < kRadixTile / 256; ++r) {
-    const uint32_t i = base + r * 256u + threadIdx.x;
-    if (i < n) atomicAdd(&c[(keys[i] >> shift) & MASK], 1u);
-  }
-  __syncthreads();
-  for (uint32_t d = threadIdx.x; d < RAD; d += 256) hist[d * ntiles + blockIdx.x] = c[d];
-}
-
-template <int B>
-__global__ __launch_bounds__(256) void k_radix_scatter_w(const uint32_t* __restrict__ kin,
-                                                         const uint32_t* __restrict__ vin,
-                                                         uint32_t* __restrict__ kout,
-                                                         uint32_t* __restrict__ vout, uint32_t n,
-                                                         int shift, uint32_t ntiles,
-                                                         const uint32_t* __restrict__ hist) {
-  constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u;
-  __shared__ uint32_t lk[kRadixTile], lv[kRadixTile];
-  __shared__ uint32_t gbase[RAD], lstart[RAD], run[RAD];
-  __shared__ uint32_t wcnt[4][RAD];
-  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  const uint32_t tile0 = blockIdx.x * (uint32_t)kRadixTile;
-  const uint32_t m = min((uint32_t)kRadixTile, n - tile0);
-  for (uint32_t d = t; d < RAD; d += 256) {
-    gbase[d] = hist[d * ntiles + blockIdx.x];
-    run[d] = 0;
-    wcnt[0][d] = wcnt[1][d] = wcnt[2][d] = wcnt[3][d] = 0;
-  }
-  __syncthreads();
-  for (uint32_t i = t; i < m; i += 256) atomicAdd(&wcnt[0][(kin[tile0 + i] >> shift) & MASK], 1u);
-  __syncthreads();
-  {  // tile-local digit offsets: exclusive scan of RAD counts, RAD / 256 per thread
-    constexpr uint32_t PER = RAD / 256;
-    uint32_t v[PER], acc = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-      v[q] = wcnt[0][t * PER + q];
-      acc += v[q];
-    }
-    uint32_t total;
-    uint32_t pre = block_excl_scan_256(acc, &total);
-#pragma unroll
-    for (uint32_t q = 0; q < PER; ++q) {
-      lstart[t * PER + q] = pre;
-      pre += v[q];
-    }
-  }
-  for (uint32_t d = t; d < RAD; d += 256) wcnt[0][d] = 0;
-  __syncthreads();
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int r = 0; r < kRadixTile / 256; ++r) {
-    const uint32_t i = r * 256u + t;
-    const bool valid = i < m;
-    const uint32_t k = valid ? kin[tile0 + i] : 0u;
-    const uint32_t v = valid ? vin[tile0 + i] : 0u;
-    const uint32_t dig = (k >> shift) & MASK;
-    uint64_t match = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const bool bit = (dig >> b) & 1u;
-      const uint64_t mb = __ballot(bit);
-      match &= bit ? mb : ~mb;
-    }
-    const uint32_t rank = __popcll(match & lt_mask);
-    if (valid && rank == 0) wcnt[w][dig] = __popcll(match);
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = lstart[dig] + run[dig] + rank;
-      for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dig];
-      lk[pos] = k;
-      lv[pos] = v;
-    }
-    __syncthreads();
-    if (valid && rank == 0) {  // the digits present this round: one updater each (lowest wave)
-      bool first = true;
-      for (uint32_t q = 0; q < w; ++q) first = first && wcnt[q][dig] == 0u;
-      if (first) run[dig] += wcnt[0][dig] + wcnt[1][dig] + wcnt[2][dig] + wcnt[3][dig];
-    }
-    __syncthreads();
-    if (valid && rank == 0) wcnt[w][dig] = 0;
-    __syncthreads();
-  }
-  for (uint32_t e = t; e < m; e += 256) {
-    const uint32_t k = lk[e];
-    const uint32_t d = (k >> shift) & MASK;
-    kout[gbase[d] + (e - lstart[d])] = k;
-    vout[gbase[d] + (e - lstart[d])] = lv[e];
-  }
-}
-
-// ---------------------------------------------------------------- onesweep (single pass) ------
-// The same stable LSD sort with one kernel per digit pass: an up-front histogram of every pass's
-// digits (one read of the keys) gives each digit's global base; the scatter kernels take tiles in
-// ticket order and get each (tile, digit)'s offset among earlier tiles from a decoupled look-back
-// over per-tile digit counts (status words as in k_scan_lb: epoch | flag | count, 64 bit).  The
-// rank of a key inside its tile is computed exactly as in k_radix_scatter_lds, so the result is
-// the same stable permutation.  Sort workspace (`hist`, u32 words):
-//   [0, 1024) ghist[4][256]   [1024, 1028) tickets   [1028, 1032) done counters   [1032] epoch
-//   [kSortStatusWord, +512 * ntiles) status[tile][256] (u64)
-// ghist, tickets and done counters are returned to zero by the last workgroup of each pass, so
-// nothing is cleared between sorts (the engine zeroes the workspace once, at allocation).
-constexpr uint32_t kSortGhist = 0, kSortTicket = 1024, kSortDone = 1028, kSortEpoch = 1032;
-
-__global__ __launch_bounds__(256) void k_os_hist(const uint32_t* __restrict__ keys, uint32_t n,
-                                                 int passes, uint32_t* __restrict__ ws) {
-  __shared__ uint32_t c[4][256];
-  const uint32_t t = threadIdx.x;
-  c[0][t] = c[1][t] = c[2][t] = c[3][t] = 0;
-  __syncthreads();
-  for (uint32_t i = blockIdx.x * 256u + t; i < n; i += gridDim.x * 256u) {
-    const uint32_t k = keys[i];
-    for (int p = 0; p < passes; ++p) atomicAdd(&c[p][(k >> (8 * p)) & 255u], 1u);
-  }
-  __syncthreads();
-  for (int p = 0; p < passes; ++p)
-    if (c[p][t]) atomicAdd(&ws[kSortGhist + p * 256 + t], c[p][t]);
-  // one epoch per sort (passes use epoch + 0..3); no workgroup of this kernel reads it
-  if (blockIdx.x == 0 && t == 0) ws[kSortEpoch] = (ws[kSortEpoch] + 4u) & kEpochMask;
-}
-
-__global__ __launch_bounds__(256) void k_os_scatter(const uint32_t* __restrict__ kin,
-                                                    const uint32_t* __restrict__ vin,
-                                                    uint32_t* __restrict__ kout,
-                                                    uint32_t* __restrict__ vout, uint32_t n,
-                                                    int pass, uint32_t* __restrict__ ws,
-                                                    uint32_t* __restrict__ err) {
-  __shared__ uint32_t lk[kRadixTile], lv[kRadixTile];
-  __shared__ uint32_t gbase[256];   // global offset of the tile's first key of each digit
-  __shared__ uint32_t lstart[256];  // tile-local offset of each digit
-  __shared__ uint32_t run[256];     // keys of each digit placed so far
-  __shared__ uint32_t wcnt[4][256];
-  __shared__ uint32_t s_tile, s_epoch, s_last;
-  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  const int shift = 8 * pass;
-  uint64_t* status = reinterpret_cast<uint64_t*>(ws + kSortStatusWord);
-  if (t == 0) {
-    s_tile = atomicAdd(&ws[kSortTicket + pass], 1u);
-    s_epoch = (ws[kSortEpoch] + (uint32_t)pass) & kEpochMask;
-  }
-  run[t] = 0;
-  wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
-  __syncthreads();
-  const uint32_t tile = s_tile, epoch = s_epoch;
-  const uint32_t ntiles = (n + kRadixTile - 1) / kRadixTile;
-  if (tile < ntiles) {
-    const uint32_t tile0 = tile * (uint32_t)kRadixTile;
-    const uint32_t m = min((uint32_t)kRadixTile, n - tile0);
-    for (uint32_t i = t; i < m; i += 256) atomicAdd(&wcnt[0][(kin[tile0 + i] >> shift) & 255u], 1u);
-    __syncthreads();
-    const uint32_t cnt = wcnt[0][t];
-    uint64_t* my = status + (size_t)tile * 256u + t;
-    status_store(my, status_pack(epoch, tile == 0 ? kStatusPrefix : kStatusAgg, cnt));
-    // look-back at once (the sooner this tile's prefix is out, the shorter its successors' walks):
-    // lane t owns digit t and reads kLookback earlier tiles' words per step
-    uint32_t excl = 0;
-    if (tile > 0) {
-      constexpr int kLookback = 8;
-      const uint64_t before0 = status_pack(epoch, kStatusPrefix, 0);  // "tile -1": empty prefix
-      int64_t j = (int64_t)tile - 1;
-      uint32_t spins = 0;
-      while (true) {
-        uint64_t v[kLookback];
-#pragma unroll
-        for (int q = 0; q < kLookback; ++q)
-          v[q] = j - q >= 0 ? status_load(status + (size_t)(j - q) * 256u + t) : before0;
-        int q = 0;
-        bool found = false;
-        for (; q < kLookback; ++q) {
-          const uint32_t f = status_flag(v[q], epoch);
-          if (f == 0u) break;
-          excl += (uint32_t)v[q];
-          if (f == kStatusPrefix) {
-            found = true;
-            break;
-          }
-        }
-        if (found) break;
-        j -= q;
-        if (q < kLookback) {  // tile j has published nothing yet
-          if (++spins > kSpinLimit) {
-            atomicOr(err, 2u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      status_store(my, status_pack(epoch, kStatusPrefix, excl + cnt));
-    }
-    {
-      uint32_t total;
-      lstart[t] = block_excl_scan_256(cnt, &total);
-    }
-    {
-      uint32_t total;
-      gbase[t] = block_excl_scan_256(ws[kSortGhist + pass * 256 + t], &total) + excl;
-    }
-    wcnt[0][t] = 0;
-    __syncthreads();
-    // stable order of the tile by digit, in LDS
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int r = 0; r < kRadixTile / 256; ++r) {
-      const uint32_t i = r * 256u + t;
-      const bool valid = i < m;
-      const uint32_t k = valid ? kin[tile0 + i] : 0u;
-      const uint32_t v = valid ? vin[tile0 + i] : 0u;
-      const uint32_t dig = (k >> shift) & 255u;
-      uint64_t match = __ballot(valid);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const bool bit = (dig >> b) & 1u;
-        const uint64_t mb = __ballot(bit);
-        match &= bit ? mb : ~mb;
-      }
-      const uint32_t rank = __popcll(match & lt_mask);
-      if (valid && rank == 0) wcnt[w][dig] = __popcll(match);
-      __syncthreads();
-      if (valid) {
-        uint32_t pos = lstart[dig] + run[dig] + rank;
-        for (uint32_t q = 0; q < w; ++q) pos += wcnt[q][dig];
-        lk[pos] = k;
-        lv[pos] = v;
-      }
-      __syncthreads();
-      run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-      wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
-      __syncthreads();
-    }
-    // write out in LDS order: entry e of digit d goes to gbase[d] + (e - lstart[d])
-    for (uint32_t e = t; e < m; e += 256) {
-      const uint32_t k = lk[e];
-      const uint32_t d = (k >> shift) & 255u;
-      const uint32_t pos = gbase[d] + (e - lstart[d]);
-      kout[pos] = k;
-      vout[pos] = lv[e];
-    }
-  }
-  // the last workgroup out returns the pass's ticket, done counter and histogram to zero
-  if (t == 0) s_last = atomicAdd(&ws[kSortDone + pass], 1u) == gridDim.x - 1 ? 1u : 0u;
-  __syncthreads();
-  if (s_last) {
-    atomicExch(&ws[kSortGhist + pass * 256 + t], 0u);
-    if (t == 0) {
-      atomicExch(&ws[kSortTicket + pass], 0u);
-      atomicExch(&ws[kSortDone + pass], 0u);
-    }
-  }
-}
-
-// KLSH_SORT=onesweep selects the single-kernel-per-pass look-back sort.  Measured on MI355X
-// (tools/ubench_sort, 23-bit keys): 86 vs 76 us at 390K keys and 1157 vs 336 us at 9.47M — the
-// look-back chains across ~1800 co-resident tiles cost more than the launches they save — so the
-// LSD passes (histogram, scan, LDS-staged scatter) stay the default.
-static bool sort_lsd() {
-  static const bool v = [] {
-    const char* e = getenv("KLSH_SORT");
-    return !(e && std::string(e) == "onesweep");
-  }();
-  return v;
-}
-
-int scan_variant() {
-  static const int v = [] {
-    const char* e = getenv("KLSH_SCAN");
-    if (!e) return 0;
-    const std::string x(e);
-    return x == "2k" ? 1 : x == "3k" ? 2 : x == "lb" ? 3 : 0;
-  }();
-  return v;
-}
-
-void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
-                uint32_t* hist, uint32_t* tile_sums, Counters* ctr, uint32_t** out_k,
-                uint32_t** out_v, hipStream_t s) {
-  uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
-  const uint32_t ntiles = (n + kRadixTile - 1) / kRadixTile;
-  const int passes = n > 1 ? (bits + 7) / 8 : 0;
-  if (!sort_lsd()) {
-    if (passes > 0) {
-      k_os_hist<<<std::min<uint32_t>(ntiles, 1024u), 256, 0, s>>>(ki, n, passes, hist);
-      for (int p = 0; p < passes; ++p) {
-        k_os_scatter<<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, p, hist, &ctr->err);
-        std::swap(ki, ko);
-        std::swap(vi, vo);
-      }
-    }
-    *out_k = ki;
-    *out_v = vi;
-    return;
-  }
-  // LSD passes: [digit][tile] histogram in the status area (the onesweep words stay intact)
-  uint32_t* h = hist + kSortStatusWord;
-  // Two passes of 9- or 10-bit digits instead of three of 8 when the key has 17..20 bits and the
-  // wider histogram stays small (KLSH_SORT_WIDE=0: always 8-bit digits)
-  static const bool wide_ok = [] {
-    const char* e = getenv("KLSH_SORT_WIDE");
-    return !(e && e[0] == '0');
-  }();
-  if (wide_ok && n > 1 && bits >= 17 && bits <= 20 && (uint64_t)ntiles * 1024u <= (1u << 20)) {
-    const int B = (bits + 1) / 2;
-    for (int shift = 0; shift < bits; shift += B) {
-      const uint32_t rad = 1u << B;
-      if (B == 9) k_radix_hist_w<9><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, h);
-      else k_radix_hist_w<10><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, h);
-      device_scan(SrcArray{h}, DstExclusive{h}, rad * ntiles, tile_sums, &ctr->total, &ctr->err, s);
-      if (B == 9) k_radix_scatter_w<9><<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, h);
-      else k_radix_scatter_w<10><<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, h);
-      std::swap(ki, ko);
-      std::swap(vi, vo);
-    }
-    *out_k = ki;
-    *out_v = vi;
-    return;
-  }
-  static const bool scatter_lds = [] {  // KLSH_SCATTER=direct: the unstaged scatter
-    const char* e = getenv("KLSH_SCATTER");
-    return !(e && std::string(e) == "direct");
-  }();
-  for (int shift = 0; shift < bits && n > 1; shift += 8) {
-    k_radix_hist<<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, h);
-    device_scan(SrcArray{h}, DstExclusive{h}, 256u * ntiles, tile_sums, &ctr->total, &ctr->err, s);
-    if (scatter_lds)
-      k_radix_scatter_lds<<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, h);
-    else
-      k_radix_scatter<<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, h);
-    std::swap(ki, ko);
-    std::swap(vi, vo);
-  }
-  *out_k = ki;
-  *out_v = vi;
+  k_compact_apply<<<ntiles, 256, 0, s>>>(slots, n, counts, out, &ctr->total, ctr, pub ? *pub : none,
+                                         rc);
 }
 
 // ============================================================================= mode C =========
@@ -1379,20 +846,22 @@ void launch_norms(const Rows& r, uint32_t n, hipStream_t s) {
   if (n) k_norms<<<(n + 255) / 256, 256, 0, s>>>(r, n);
 }
 
+// One row per wave-pass, grid-strided: a launch's work-items must stay below 2^32 (C5's result,
+// 9.98M rows x 512, is 5.1e9 floats — a thread per float wrapped and dropped 2^32 of them).
 __global__ __launch_bounds__(256) void k_gather_rows(Rows r, const uint32_t* __restrict__ order,
                                                      uint32_t n, float* __restrict__ out) {
-  const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  const uint64_t total = (uint64_t)n * (uint64_t)r.d;
-  if (t >= total) return;
-  const uint32_t i = (uint32_t)(t / (uint64_t)r.d);
-  const uint32_t k = (uint32_t)(t % (uint64_t)r.d);
-  out[t] = r.x[(size_t)order[i] * r.dp + k];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6), nwaves = gridDim.x * 4u;
+  for (uint32_t i = wave; i < n; i += nwaves) {
+    const float* src = r.x + (size_t)order[i] * r.dp;
+    float* dst = out + (size_t)i * r.d;
+    for (int k = (int)lane; k < r.d; k += 64) dst[k] = src[k];
+  }
 }
 
 void launch_gather_rows(const Rows& r, const uint32_t* order, uint32_t n, float* out,
                         hipStream_t s) {
-  const uint64_t total = (uint64_t)n * (uint64_t)r.d;
-  if (total) k_gather_rows<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(r, order, n, out);
+  if (n) k_gather_rows<<<std::min<uint32_t>((n + 3) / 4, 65536u), 256, 0, s>>>(r, order, n, out);
 }
 
 __global__ void k_fp_selftest(const float* a, const float* b, uint32_t n, float* so, float* dv) {

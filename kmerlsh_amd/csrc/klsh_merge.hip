@@ -42,11 +42,9 @@ __device__ __forceinline__ void wave_lds_fence() {
   // from moving LDS accesses across this point (no wait for outstanding global stores)
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
-// KLSH_GRAM_TILES=0 at build time keeps the exact all-pairs VALU tiles everywhere (A/B).
-#ifndef KLSH_GRAM_TILES
-#define KLSH_GRAM_TILES 1
-#endif
-constexpr bool kGramTiles = KLSH_GRAM_TILES != 0;
+// The all-pairs decisions of 65..896-row runs go through the certified MFMA Gram screen when the
+// decider has a fast path and d is a multiple of 16 (else the exact VALU tiles).
+constexpr bool kGramTiles = true;
 
 // Merge profiling (diagnostics build only: -DKLSH_MERGE_PROF, make prof): per size class, the
 // runs, rows, merges and wall-clock ticks (100 MHz) of each phase, summed over the call.
@@ -163,38 +161,8 @@ __device__ __forceinline__ float dot_lds_lds(const float* a, const float* b) {
   return s;
 }
 
-// ---------------------------------------------------------------------------- segments -----
-struct SrcHead {  // 1 at the first position of every run of equal keys in [lo, lo + n)
-  const uint32_t* key;
-  uint32_t lo;
-  __device__ uint32_t operator()(uint32_t i) const {
-    return (i == 0 || key[lo + i] != key[lo + i - 1]) ? 1u : 0u;
-  }
-};
-struct DstSegStart {
-  uint32_t* seg;
-  uint32_t lo;
-  __device__ void operator()(uint32_t i, uint32_t prefix, uint32_t v) const {
-    if (v) seg[prefix] = lo + i;
-  }
-};
-
 __device__ __forceinline__ int size_class(uint32_t b) {  // G = 2 << class lanes per run
   return b <= 2 ? 0 : b <= 4 ? 1 : b <= 8 ? 2 : b <= 16 ? 3 : b <= 32 ? 4 : 5;
-}
-
-// Queue a long run (rare) to the big / huge / nestedCluster list.
-__device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucket_thr,
-                                               const MergeWork& w, Counters* ctr) {
-  if (bucket_thr >= 0 && b > (uint32_t)bucket_thr) {  // cluster.cc:286 -> nestedCluster
-    w.over[atomicAdd(&ctr->n_over, 1u)] = make_uint2(p, b);
-  } else if (b <= (uint32_t)kBigRows[kBigClasses - 1]) {
-    int c = 0;
-    while (b > (uint32_t)kBigRows[c]) ++c;
-    w.big[c][atomicAdd(&ctr->n_big[c], 1u)] = make_uint2(p, b);
-  } else {
-    w.huge[atomicAdd(&ctr->n_huge, 1u)] = make_uint2(p, b);
-  }
 }
 
 // --------------------------------------------------------------------- G-lane groups -----
@@ -202,23 +170,8 @@ __device__ __forceinline__ void queue_long_run(uint32_t p, uint32_t b, int bucke
 // g of its run and owns row id g: row in registers x[] and at LDS row `lane`.
 // One batch: run (p, b) of lane's group, lane's slot already loaded (the caller pipelines those
 // loads one batch ahead, so only the row gather is exposed here).
-#ifndef KLSH_ROW_PREFETCH
-#define KLSH_ROW_PREFETCH 0
-#endif
-constexpr bool kRowPrefetch = KLSH_ROW_PREFETCH != 0;
-#ifndef KLSH_LAZY_META
-#define KLSH_LAZY_META 1
-#endif
-constexpr bool kLazyMeta = KLSH_LAZY_META != 0;  // -DKLSH_LAZY_META=0: eager loads (A/B build)
-#ifndef KLSH_NORM_FROM_ROW
-#define KLSH_NORM_FROM_ROW 1
-#endif
-constexpr bool kNormFromRow = KLSH_NORM_FROM_ROW != 0;  // -DKLSH_NORM_FROM_ROW=0: read r.nrm
-
-template <int G, int D, class Prefetch>
+template <int G, int D>
 __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
-                                            float4 (&rb)[kRowPrefetch ? D / 4 : 1],
-                                            Prefetch prefetch,
                                             uint32_t* slots, const Decider& dc, const Rows& r,
                                             float* lds, uint32_t* dlist, Counters* ctr) {
   constexpr int ST = D + 4;  // padded row stride: 16 lanes of a ds_read_b128 hit distinct banks
@@ -231,33 +184,20 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
   [[maybe_unused]] uint64_t sp1 = 0, sp2 = 0, sp3 = 0;
   {
     const bool valid = g < b;
-    // the row's norm: recomputed from the row (the same sequential chain that made the cached
-    // value, distance.cc:33-34, so the same bits) instead of a random 4-B read of r.nrm
-    float nrm = (!kNormFromRow && valid) ? r.nrm[slot] : 0.0f;
     // member count / list ends: only a merge needs them, and most batches have none — they are
     // loaded after the pairwise decisions, by waves that found a matching pair (saves three
     // random 4-B reads per row, as much traffic as the row itself)
     uint32_t cnt = 0u, hd = 0u, tl = 0u;
-    if (!kLazyMeta && valid) {
-      cnt = r.cnt[slot];
-      hd = r.head[slot];
-      tl = r.tail[slot];
-    }
-    if constexpr (kRowPrefetch) {
-      store_rows<D>(rb, lds);  // rows gathered one batch ahead -> LDS row l = lane l's row
-    } else {
-      stage_rows<D>(r.x, r.dp, slot, valid, lds);  // row of lane l -> LDS row l, coalesced
-    }
-    if constexpr (kRowPrefetch) prefetch();  // the next batch's row loads fly during this batch
+    stage_rows<D>(r.x, r.dp, slot, valid, lds);  // row of lane l -> LDS row l, coalesced
     wave_lds_fence();
     float x[D];
     load_row<D>(myrow, x);
-    if constexpr (kNormFromRow) {
-      nrm = 0.0f;
+    // the row's norm: recomputed from the row (the same sequential chain that made the cached
+    // value, distance.cc:33-34, so the same bits) instead of a random 4-B read of r.nrm
+    float nrm = 0.0f;
 #pragma unroll
-      for (int k = 0; k < D; ++k) nrm = nrm + x[k] * x[k];
-      if (!valid) nrm = 0.0f;
-    }
+    for (int k = 0; k < D; ++k) nrm = nrm + x[k] * x[k];
+    if (!valid) nrm = 0.0f;
     float sq = __builtin_sqrtf(nrm);  // this row's sqrtf(|x|^2), distance.cc:37
     const uint32_t bmax = wave_max(b);
 #ifdef KLSH_MERGE_PROF
@@ -296,7 +236,7 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
       share(k + 1, h1);
     }
 
-    if (kLazyMeta && __ballot(valid && full != 0ull)) {  // some run of the wave merges
+    if (__ballot(valid && full != 0ull)) {  // some run of the wave merges
       if (valid) {
         cnt = r.cnt[slot];
         hd = r.head[slot];
@@ -400,47 +340,6 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
 #endif
 }
 
-// One lane per run: runs of 2..64 rows go to their size-class list, longer ones to the big /
-// huge / nestedCluster lists.  Offsets are aggregated per wave (ballot) and per workgroup (LDS),
-// so each workgroup issues one global atomic per class.
-__global__ __launch_bounds__(1024) void k_classify(const uint32_t* __restrict__ seg, uint32_t hi,
-                                                   int bucket_thr, MergeWork w, Counters* ctr) {
-  __shared__ uint32_t bcnt[kGroupClasses], bbase[kGroupClasses];
-  const uint32_t nseg = __hip_atomic_load(&ctr->n_seg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (blockIdx.x * 1024u >= nseg) return;  // whole workgroup past the end
-  const uint32_t t = threadIdx.x, lane = t & 63u;
-  const uint64_t lt = lanes_below(lane);
-  if (t < (uint32_t)kGroupClasses) bcnt[t] = 0u;
-  __syncthreads();
-  const uint32_t s = blockIdx.x * 1024u + t;
-  uint32_t p = 0, b = 0;
-  int cls = -1;
-  if (s < nseg) {
-    p = seg[s];
-    b = ((s + 1 < nseg) ? seg[s + 1] : hi) - p;
-    if ((bucket_thr >= 0 && b > (uint32_t)bucket_thr) || b > 64u) {
-      queue_long_run(p, b, bucket_thr, w, ctr);
-    } else if (b >= 2) {
-      cls = size_class(b);
-    }
-  }
-  uint32_t myoff = 0;
-#pragma unroll
-  for (int c = 0; c < kGroupClasses; ++c) {
-    const uint64_t m = __ballot(cls == c);
-    if (m == 0ull) continue;
-    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)m) - 1);
-    uint32_t woff = 0;
-    if (lane == leader) woff = atomicAdd(&bcnt[c], (uint32_t)__popcll(m));
-    woff = shfl32(woff, leader);
-    if (cls == c) myoff = woff + (uint32_t)__popcll(m & lt);
-  }
-  __syncthreads();
-  if (t < (uint32_t)kGroupClasses && bcnt[t]) bbase[t] = atomicAdd(&ctr->n_cls[t], bcnt[t]);
-  __syncthreads();
-  if (cls >= 0) w.cls[cls][bbase[cls] + myoff] = make_uint2(p, b);
-}
-
 // ------------------------------------------------- all small-run classes in one launch -----
 // Runs of 2..64 rows of every size class in ONE persistent launch: the batches of all classes
 // (a batch = one wave's 64/G runs of class G; 64 runs of 2 for the pair class) are numbered in
@@ -470,18 +369,12 @@ __device__ __forceinline__ void pair_batch(const uint2* __restrict__ list, uint3
     float dot = 0.0f;
 #pragma unroll
     for (int q = 0; q < D; ++q) dot = dot + x1[q] * x0[q];  // cosine(c[1], c[0]), in order
-    float n0, n1;
-    if constexpr (kNormFromRow) {  // recomputed from the rows in registers (same chain, same bits)
-      n0 = 0.0f;
-      n1 = 0.0f;
+    // the norms, recomputed from the rows in registers (the cached chain, distance.cc:33-34)
+    float n0 = 0.0f, n1 = 0.0f;
 #pragma unroll
-      for (int q = 0; q < D; ++q) {
-        n0 = n0 + x0[q] * x0[q];
-        n1 = n1 + x1[q] * x1[q];
-      }
-    } else {
-      n0 = r.nrm[s0];
-      n1 = r.nrm[s1];
+    for (int q = 0; q < D; ++q) {
+      n0 = n0 + x0[q] * x0[q];
+      n1 = n1 + x1[q] * x1[q];
     }
     if (decide(dc, dot, __builtin_sqrtf(n1) * __builtin_sqrtf(n0))) {
       merged = true;
@@ -520,7 +413,7 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
   uint32_t n[NC], nb[NC], start[NC + 1];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
-    n[c] = __hip_atomic_load(&ctr->n_cls[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    n[c] = __hip_atomic_load(&w.rc->n_cls[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   nb[0] = (n[0] + 63u) / 64u;
   nb[1] = batches_of<4>(n[1]);
   nb[2] = batches_of<8>(n[2]);
@@ -563,7 +456,6 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
       if (g < e.y) slot = slots[e.x + g];
     }
   };
-  float4 rb[1];
   uint2 e;
   uint32_t slot;
   fetch(wave, e, slot);
@@ -574,26 +466,17 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
     int c;
     uint32_t bi;
     locate(t, c, bi);
-    auto none = [] {};
     switch (c) {  // wave-uniform
       case 0: pair_batch<D>(w.cls[0], n[0], bi, slots, dc, r, ctr, w.dlist); break;
-      case 1: merge_batch<4, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
-      case 2: merge_batch<8, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
-      case 3: merge_batch<16, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
-      case 4: merge_batch<32, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
-      default: merge_batch<64, D>(e.x, e.y, slot, rb, none, slots, dc, r, lds, w.dlist, ctr); break;
+      case 1: merge_batch<4, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
+      case 2: merge_batch<8, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
+      case 3: merge_batch<16, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
+      case 4: merge_batch<32, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
+      default: merge_batch<64, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
     }
     e = e_next;
     slot = slot_next;
   }
-}
-
-static bool big384_rows_lds() {  // KLSH_BIG384_LDS=0: 129..384-row runs read rows from L2
-  static const bool v = [] {
-    const char* e = getenv("KLSH_BIG384_LDS");
-    return !(e && e[0] == '0');
-  }();
-  return v;
 }
 
 template <int D>
@@ -603,37 +486,39 @@ __global__ __launch_bounds__(64) void k_merge_small(MergeWork w, uint32_t* __res
   small_loop<D>(w, slots, dc, r, ctr, lds, blockIdx.x, gridDim.x);
 }
 
-static bool small_fused() {  // KLSH_SMALL=split: one kernel per size class on the streams (A/B)
-  static const bool v = [] {
-    const char* e = getenv("KLSH_SMALL");
-    return !(e && std::string(e) == "split");
-  }();
-  return v;
-}
-
-// Runs of equal keys found and classified in one pass (replaces the head-flag scan + k_classify):
-// a tile of 4096 positions is read coalesced (position k*256 + t by thread t), head flags become
-// a 4096-bit LDS bitmap (wave ballots), each head finds its run's end as the next set bit (the
-// last run of the tile looks past the tile end, one wave, 64 keys per step), and the runs go to
-// their class lists with one global atomic per class per workgroup.
-constexpr int kRunTile = 4096;
+// Runs of equal keys found and listed by size class in one pass: a tile of 16384 positions is
+// read coalesced (position k*256 + t by thread t), head flags become a 16384-bit LDS bitmap (wave
+// ballots), each head finds its run's end as the next set bit (the last run of the tile looks past
+// the tile end, one wave, 64 keys per step).  Runs are counted per list in LDS, each list's range
+// is reserved with ONE global add per workgroup (every counter on a 128-B line of its own:
+// RunCounters), and the entries are written in a second sweep over the bitmap.  Entries within a
+// list are in no particular order; every merge result is positional.
+constexpr int kRunTile = 16384;
+constexpr int kRunLists = kGroupClasses + kBigClasses + 2;  // small classes, big classes, huge, over
 __global__ __launch_bounds__(256) void k_runs(const uint32_t* __restrict__ key, uint32_t lo,
-                                              uint32_t n, int bucket_thr, MergeWork w,
-                                              Counters* ctr) {
+                                              uint32_t n, int bucket_thr, MergeWork w) {
   __shared__ uint64_t hb[kRunTile / 64];  // head bitmap of the tile, word = 64 positions
-  __shared__ uint32_t bcnt[kGroupClasses + 1], bbase[kGroupClasses + 1];
+  __shared__ uint32_t lcnt[kRunLists + 1], lbase[kRunLists], lfill[kRunLists];
   __shared__ uint32_t s_tail_end;  // first head at or after the tile end (or n)
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t T0 = blockIdx.x * (uint32_t)kRunTile;
-  if (t <= (uint32_t)kGroupClasses) bcnt[t] = 0u;
+  if (t <= (uint32_t)kRunLists) lcnt[t] = 0u;
+  if (t < (uint32_t)kRunLists) lfill[t] = 0u;
   const uint32_t* kp = key + lo;
+  for (int k0 = 0; k0 < kRunTile / 256; k0 += 16) {
+    uint32_t a[16], b[16];
 #pragma unroll
-  for (int k = 0; k < kRunTile / 256; ++k) {
-    const uint32_t i = T0 + k * 256u + t;
-    bool head = false;
-    if (i < n) head = i == 0 || kp[i] != kp[i - 1];
-    const uint64_t m = __ballot(head);
-    if (lane == 0) hb[k * 4 + wv] = m;
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t i = T0 + (uint32_t)(k0 + k) * 256u + t;
+      a[k] = i < n ? kp[i] : 0u;
+      b[k] = (i < n && i > 0) ? kp[i - 1] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t i = T0 + (uint32_t)(k0 + k) * 256u + t;
+      const uint64_t m = __ballot(i < n && (i == 0 || a[k] != b[k]));
+      if (lane == 0) hb[(k0 + k) * 4 + wv] = m;
+    }
   }
   if (wv == 0) {  // the end of the tile's last run: the first head at or after T0 + kRunTile
     uint32_t j = T0 + (uint32_t)kRunTile, end = n;
@@ -651,152 +536,58 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t* __restrict__ key, 
   }
   __syncthreads();
   const uint32_t tail_end = s_tail_end;
-  uint32_t bl[kRunTile / 256];  // run length of the head at my position k*256 + t, 0 if none
-  int cl[kRunTile / 256];
-  uint32_t off[kRunTile / 256];
-  uint32_t heads = 0;
-#pragma unroll
-  for (int k = 0; k < kRunTile / 256; ++k) {
-    const uint32_t q = k * 256u + t;  // tile-local position
-    bl[k] = 0u;
-    cl[k] = -1;
-    off[k] = 0u;
-    if ((hb[q >> 6] >> (q & 63u)) & 1ull) {
-      uint32_t wi = q >> 6;
-      uint64_t m = hb[wi] & ~((2ull << (q & 63u)) - 1ull);  // heads after q in its word
-      while (!m && ++wi < (uint32_t)(kRunTile / 64)) m = hb[wi];
-      const uint32_t next = m ? T0 + wi * 64u + (uint32_t)__builtin_ctzll(m) : tail_end;
-      const uint32_t b = next - (T0 + q);
-      bl[k] = b;
-      ++heads;
-      if ((bucket_thr >= 0 && b > (uint32_t)bucket_thr) || b > 64u) {
-        queue_long_run(lo + T0 + q, b, bucket_thr, w, ctr);
-      } else if (b >= 2) {
-        cl[k] = size_class(b);
-        off[k] = atomicAdd(&bcnt[cl[k]], 1u);
-      }
+  // the run starting at tile position q (a head): its length and list (-1: a single row)
+  auto run_at = [&](uint32_t q, uint32_t& b) -> int {
+    uint32_t wi = q >> 6;
+    uint64_t m = hb[wi] & ~((2ull << (q & 63u)) - 1ull);  // heads after q in its word
+    while (!m && ++wi < (uint32_t)(kRunTile / 64)) m = hb[wi];
+    const uint32_t next = m ? T0 + wi * 64u + (uint32_t)__builtin_ctzll(m) : tail_end;
+    b = next - (T0 + q);
+    if (bucket_thr >= 0 && b > (uint32_t)bucket_thr) return kRunLists - 1;  // cluster.cc:286
+    if (b > 64u) {
+      if (b > (uint32_t)kBigRows[kBigClasses - 1]) return kRunLists - 2;
+      int c = 0;
+      while (b > (uint32_t)kBigRows[c]) ++c;
+      return kGroupClasses + c;
     }
-  }
-  // heads of the workgroup (statistics: ctr->n_seg = runs)
-  {
-    uint32_t hsum = heads;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) hsum += __shfl_xor(hsum, o, 64);
-    if (lane == 0 && hsum) atomicAdd(&bcnt[kGroupClasses], hsum);
-  }
-  __syncthreads();
-  if (t < (uint32_t)kGroupClasses && bcnt[t]) bbase[t] = atomicAdd(&ctr->n_cls[t], bcnt[t]);
-  if (t == (uint32_t)kGroupClasses && bcnt[t]) atomicAdd(&ctr->n_seg, bcnt[t]);
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kRunTile / 256; ++k)
-    if (cl[k] >= 0) w.cls[cl[k]][bbase[cl[k]] + off[k]] = make_uint2(lo + T0 + k * 256u + t, bl[k]);
-}
-
-static bool runs_via_scan() {  // KLSH_RUNS=scan: head-flag scan + k_classify (A/B)
-  static const bool v = [] {
-    const char* e = getenv("KLSH_RUNS");
-    return e && std::string(e) == "scan";
-  }();
-  return v;
-}
-
-// One wave per batch of 64/G runs of one size class (persistent over the class list).
-// One wave per batch of 64/G runs of one size class (persistent over the class list).  The list
-// entry and the slots of the NEXT batch are loaded while the current one is merged.
-template <int G, int D>
-__global__ __launch_bounds__(64) void k_merge_group(const uint2* __restrict__ list, int cls,
-                                                    uint32_t* __restrict__ slots, Decider dc,
-                                                    Rows r, Counters* ctr, uint32_t* dlist) {
-  __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
-  constexpr uint32_t NG = 64 / G;
-  const uint32_t n = __hip_atomic_load(&ctr->n_cls[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nb = (n + NG - 1) / NG;
-  const uint32_t g = threadIdx.x & (G - 1), grp = threadIdx.x / G;
-  auto entry = [&](uint32_t bi) -> uint2 {
-    const uint32_t k = bi * NG + grp;
-    return (bi < nb && k < n) ? list[k] : make_uint2(0u, 0u);
+    return b >= 2 ? size_class(b) : -1;
   };
-  uint2 e = entry(blockIdx.x);
-  uint32_t slot = g < e.y ? slots[e.x + g] : 0u;
-  float4 rb[kRowPrefetch ? D / 4 : 1];  // this wave's 64 rows, loaded one batch ahead
-  if constexpr (kRowPrefetch) gather_rows<D>(r.x, r.dp, slot, g < e.y, rb);
-  uint2 e_next = entry(blockIdx.x + gridDim.x);
-  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
-    const uint32_t slot_next = g < e_next.y ? slots[e_next.x + g] : 0u;
-    const uint2 e_next2 = entry(bi + 2 * gridDim.x);
-    merge_batch<G, D>(e.x, e.y, slot, rb,
-                      [&] {
-                        if constexpr (kRowPrefetch)
-                          gather_rows<D>(r.x, r.dp, slot_next, g < e_next.y, rb);
-                      },
-                      slots, dc, r, lds, dlist, ctr);
-    e = e_next;
-    slot = slot_next;
-    e_next = e_next2;
+  uint32_t heads = 0;
+  for (int k = 0; k < kRunTile / 256; ++k) {
+    const uint32_t q = (uint32_t)k * 256u + t;
+    if ((hb[q >> 6] >> (q & 63u)) & 1ull) {
+      uint32_t b;
+      const int l = run_at(q, b);
+      ++heads;
+      if (l >= 0) atomicAdd(&lcnt[l], 1u);
+    }
   }
-}
-
-// Runs of exactly 2 rows (the commonest run): p_cluster visits i = 1 once — if row 1 matches
-// row 0, row 0 becomes SetConsensus(row 1, row 0) and row 1 dies.  One lane per run, both rows in
-// registers, no LDS and no cross-lane traffic.
-template <int D>
-__global__ __launch_bounds__(256) void k_merge_pair(const uint2* __restrict__ list, int cls,
-                                                   uint32_t* __restrict__ slots, Decider dc,
-                                                   Rows r, Counters* ctr, uint32_t* dlist) {
-  const uint32_t n = __hip_atomic_load(&ctr->n_cls[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (uint32_t k0 = blockIdx.x * 256u; k0 < n; k0 += gridDim.x * 256u) {  // uniform per block
-    const uint32_t k = k0 + threadIdx.x;
-    bool merged = false;
-    uint32_t s0 = 0;
-    if (k < n) {
-      const uint2 e = list[k];
-      s0 = slots[e.x];
-      const uint32_t s1 = slots[e.x + 1];
-      float x0[D], x1[D];
-      load_row<D>(r.x + (size_t)s0 * r.dp, x0);
-      load_row<D>(r.x + (size_t)s1 * r.dp, x1);
-      float dot = 0.0f;
 #pragma unroll
-      for (int q = 0; q < D; ++q) dot = dot + x1[q] * x0[q];  // cosine(c[1], c[0]), in order
-      float n0, n1;
-    if constexpr (kNormFromRow) {  // recomputed from the rows in registers (same chain, same bits)
-      n0 = 0.0f;
-      n1 = 0.0f;
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        n0 = n0 + x0[q] * x0[q];
-        n1 = n1 + x1[q] * x1[q];
-      }
-    } else {
-      n0 = r.nrm[s0];
-      n1 = r.nrm[s1];
+  for (int o = 32; o > 0; o >>= 1) heads += __shfl_xor(heads, o, 64);
+  if (lane == 0 && heads) atomicAdd(&lcnt[kRunLists], heads);
+  __syncthreads();
+  auto counter = [&](int l) -> uint32_t* {
+    RunCounters* rc = w.rc;
+    return l < kGroupClasses ? &rc->n_cls[l].v
+           : l < kGroupClasses + kBigClasses ? &rc->n_big[l - kGroupClasses].v
+           : l == kRunLists - 2 ? &rc->n_huge.v : &rc->n_over.v;
+  };
+  if (t < (uint32_t)kRunLists && lcnt[t]) lbase[t] = atomicAdd(counter((int)t), lcnt[t]);
+  if (t == (uint32_t)kRunLists && lcnt[t]) atomicAdd(&w.rc->n_seg.v, lcnt[t]);
+  __syncthreads();
+  for (int k = 0; k < kRunTile / 256; ++k) {
+    const uint32_t q = (uint32_t)k * 256u + t;
+    if ((hb[q >> 6] >> (q & 63u)) & 1ull) {
+      uint32_t b;
+      const int l = run_at(q, b);
+      if (l < 0) continue;
+      const uint32_t at = lbase[l] + atomicAdd(&lfill[l], 1u);
+      const uint2 e = make_uint2(lo + T0 + q, b);
+      if (l < kGroupClasses) w.cls[l][at] = e;
+      else if (l < kGroupClasses + kBigClasses) w.big[l - kGroupClasses][at] = e;
+      else if (l == kRunLists - 2) w.huge[at] = e;
+      else w.over[at] = e;
     }
-      if (decide(dc, dot, __builtin_sqrtf(n1) * __builtin_sqrtf(n0))) {
-        merged = true;
-        const uint32_t ca = r.cnt[s1], cb = r.cnt[s0];  // current = row 1, candidate = row 0
-        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
-        float nn = 0.0f;
-        float* xo = r.x + (size_t)s0 * r.dp;
-#pragma unroll
-        for (int q = 0; q < D; q += 4) {
-          float4 v;
-          v.x = consensus(x1[q], fa, x0[q], fb, fn);
-          v.y = consensus(x1[q + 1], fa, x0[q + 1], fb, fn);
-          v.z = consensus(x1[q + 2], fa, x0[q + 2], fb, fn);
-          v.w = consensus(x1[q + 3], fa, x0[q + 3], fb, fn);
-          nn = nn + v.x * v.x;
-          nn = nn + v.y * v.y;
-          nn = nn + v.z * v.z;
-          nn = nn + v.w * v.w;
-          *reinterpret_cast<float4*>(xo + q) = v;
-        }
-        r.nrm[s0] = nn;
-        link_members(r, s1, s0);  // ids_current ++ ids_candidate; cnt[s1] = 0
-        slots[e.x + 1] = kInvalid;
-      }
-    }
-    if (dlist) append_slot(merged, s0, dlist, &ctr->n_delta);
   }
 }
 
@@ -1313,10 +1104,11 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
 template <int D, int RB, int NT, bool ROWS_LDS>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RB <= 192 ? 2 : 1))) void k_merge_big(const uint2* __restrict__ list, int cls,
                                                   uint32_t* __restrict__ slots, Decider dc,
-                                                  Rows r, Counters* ctr, uint32_t* dlist) {
+                                                  Rows r, Counters* ctr, uint32_t* dlist,
+                                                  RunCounters* rc) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t count =
-      __hip_atomic_load(&ctr->n_big[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_load(&rc->n_big[cls].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   big_runs<D, RB, NT, ROWS_LDS>(list, cls, count, blockIdx.x, gridDim.x, slots, dc, r, ctr, dlist,
                                 smem);
 }
@@ -1333,7 +1125,7 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
     uint32_t cnt[kBigClasses];
 #pragma unroll
     for (int c = 0; c < kBigClasses; ++c)
-      cnt[c] = __hip_atomic_load(&ctr->n_big[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      cnt[c] = __hip_atomic_load(&w.rc->n_big[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // one index space, longest class first: 385..896, 193..384, 129..192, 65..128
     const uint32_t a3 = cnt[3], a2 = a3 + cnt[2], a1 = a2 + cnt[1], total = a1 + cnt[0];
     for (uint32_t li = blockIdx.x; li < total; li += nbig) {  // block-uniform
@@ -1363,10 +1155,7 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
 // from memory, one exact sequential dot product each), and the first hit of the chunk is found
 // by a ballot + cross-wave min.  The run's slots and sqrtf(norms) live in LDS when they fit.
 constexpr int kHugeNT = 512;
-#ifndef KLSH_HUGE_KB
-#define KLSH_HUGE_KB 8
-#endif
-constexpr int kHugeKB = KLSH_HUGE_KB;  // visited rows tested per pass (half at d = 64)
+constexpr int kHugeKB = 8;  // visited rows tested per pass (half at d = 64); 16 measured the same
 constexpr uint32_t kHugeLdsRows = 8192;
 
 template <int D>  // D: d at compile time (unrolled dots), 0 = any d
@@ -1595,13 +1384,12 @@ static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, 
   }();
   (void)lds_ok;
   uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
-  if (w.hint[kBigClasses]) g = std::min(g, w.hint[kBigClasses]);
   switch (r.d) {
-    case 8: k_merge_huge<8><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr); break;
-    case 16: k_merge_huge<16><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr); break;
-    case 32: k_merge_huge<32><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr); break;
-    case 64: k_merge_huge<64><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr); break;
-    default: k_merge_huge<0><<<g, kHugeNT, lds, s>>>(w.huge, &ctr->n_huge, slots, dc, r, w, ctr);
+    case 8: k_merge_huge<8><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr); break;
+    case 16: k_merge_huge<16><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr); break;
+    case 32: k_merge_huge<32><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr); break;
+    case 64: k_merge_huge<64><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr); break;
+    default: k_merge_huge<0><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr);
   }
 }
 
@@ -1783,10 +1571,11 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
 template <int G>
 __global__ __launch_bounds__(64) void k_merge_group_wide(const uint2* __restrict__ list, int cls,
                                                          uint32_t* __restrict__ slots, Decider dc,
-                                                         Rows r, Counters* ctr, uint32_t* dlist) {
+                                                         Rows r, Counters* ctr, uint32_t* dlist,
+                                                         RunCounters* rc) {
   __shared__ __attribute__((aligned(16))) float tile[64 * (kWideKC + 4)];
   constexpr uint32_t NG = 64 / G;
-  const uint32_t n = __hip_atomic_load(&ctr->n_cls[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t n = __hip_atomic_load(&rc->n_cls[cls].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nb = (n + NG - 1) / NG;
   const uint32_t g = threadIdx.x & (G - 1), grp = threadIdx.x / G;
   for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
@@ -1815,7 +1604,8 @@ struct BigWideLayout {
 template <int RB, int NT, int KC>
 __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__ list, int cls,
                                                        uint32_t* __restrict__ slots, Decider dc,
-                                                       Rows r, Counters* ctr, uint32_t* dlist) {
+                                                       Rows r, Counters* ctr, uint32_t* dlist,
+                                                       RunCounters* rc) {
   using L = BigWideLayout<RB, NT, KC>;
   constexpr int W = L::W, NW = L::NW, STB = L::STB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1832,7 +1622,7 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__
   float* ctile = reinterpret_cast<float*>(smem + L::tiles) + wv * 64 * STB;  // this wave's
   const int d = r.d, dp = r.dp;
   const uint32_t count =
-      __hip_atomic_load(&ctr->n_big[cls], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_load(&rc->n_big[cls].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   auto row_ptr = [&](uint32_t a) -> const float* { return r.x + (size_t)slot[a] * dp; };
 
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
@@ -1971,23 +1761,19 @@ static void launch_big(const MergeWork& w, int c, uint32_t* slots, const Decider
   }();
   (void)lds_ok;
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
-  uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
-  if (w.hint[c]) g = std::min(g, w.hint[c]);
-  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist);
+  const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
+  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist,
+                                                           w.rc);
 }
 
-// Fork the size-class kernels onto the auxiliary streams (after k_classify on s) and join them
-// back into s.  Every class writes disjoint runs, so the order between classes is free.
+// Fork the size-class kernels onto the auxiliary streams (after k_runs on s) and join them back
+// into s.  Every class writes disjoint runs, so the order between classes is free.
 struct Fork {
   const MergeWork& w;
   hipStream_t s;
   bool on;
   Fork(const MergeWork& w_, hipStream_t s_) : w(w_), s(s_) {
-    static const bool enabled = [] {
-      const char* e = getenv("KLSH_MERGE_STREAMS");
-      return !(e && e[0] == '0');
-    }();
-    on = enabled && w.aux[0] != nullptr;
+    on = w.aux[0] != nullptr;
     if (!on) return;
     (void)hipEventRecord(w.fork, s);
     for (int i = 0; i < kMergeStreams; ++i) (void)hipStreamWaitEvent(w.aux[i], w.fork, 0);
@@ -2002,24 +1788,14 @@ struct Fork {
   }
 };
 
-static uint32_t pair_grid(uint32_t n) {  // one lane per run of 2: at most n / 2 runs
-  return (uint32_t)std::min<uint64_t>(4096, (n / 2 + 255) / 256 + 1);
-}
+// Iterations below this many positions run every merge class in ONE launch (k_merge_tail) on the
+// main stream: there the cross-stream fork/join (~35 us) costs more than the overlap buys.
+constexpr uint32_t kTailMergeMax = 1u << 20;
 
 template <int D>
-static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
-                          uint32_t* slots, const Decider& dc, const MergeWork& w, Counters* ctr,
-                          uint32_t n, hipStream_t s) {
-  if (runs_via_scan()) k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
-  // Persistent grids: run counts live on the device; each grid strides over its list.
-  auto grid = [&](int c, uint32_t per_wave) {
-    return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
-  };
-  static const uint32_t tail_max = [] {  // KLSH_TAIL_MERGE: positions below which one launch
-    const char* e = getenv("KLSH_TAIL_MERGE");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 20);
-  }();
-  if (n < tail_max && small_fused()) {
+static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, const MergeWork& w,
+                          Counters* ctr, uint32_t n, hipStream_t s) {
+  if (n < kTailMergeMax) {
     using L896 = BigLayout<D, 896, false>;
     using L384 = BigLayout<D, 384, true>;
     using L192 = BigLayout<D, 192, true>;
@@ -2038,48 +1814,19 @@ static void launch_groups(const Rows& r, const uint32_t* seg, uint32_t hi, int b
   const Fork f(w, s);
   // longest walks first on each stream; the longest runs (few, long walks) on the main stream,
   // concurrent with the auxiliary ones (it waits for them at the join)
-  if (big384_rows_lds())
-    launch_big<D, 384, 256, true>(w, 2, slots, dc, r, ctr, n, f.lane(0));
-  else
-    launch_big<D, 384, 256, false>(w, 2, slots, dc, r, ctr, n, f.lane(0));
+  launch_big<D, 384, 256, true>(w, 2, slots, dc, r, ctr, n, f.lane(0));
   // many 385..896-row runs (w.big896_aux): they go on aux 2, ahead of the small runs, instead of
   // in front of the >896-row runs on the main stream — serialised, the two long-walk classes
   // make the main stream the critical path (C4 1794 -> 1432 ms); with a handful of them (C2)
   // the main stream is the better place (measured 281-285 vs 284-294 ms)
-  launch_big<D, 896, 256, false>(w, 3, slots, dc, r, ctr, n,
-                                 f.on ? (w.big896_aux ? f.lane(2) : s) : f.lane(0));
-  launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
-  static const bool big128_wide = [] {  // KLSH_BIG128_NT=256: 4 waves per 65..128-row run (A/B)
-    const char* e = getenv("KLSH_BIG128_NT");
-    return e && atoi(e) == 256;
-  }();
+  launch_big<D, 896, 256, false>(w, 3, slots, dc, r, ctr, n, w.big896_aux ? f.lane(2) : s);
+  launch_huge(w, slots, dc, r, ctr, n, s);
   // 129..192 rows: two workgroups per CU (62 KB of LDS at d = 64, VGPRs capped at 256 like the
   // 65..128 class), ahead of 65..128 on aux 1
   launch_big<D, 192, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(1));
-  if (big128_wide)
-    launch_big<D, 128, 256, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
-  else
-    launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
-  if (small_fused()) {
-    // a persistent grid: 2x the batches of the previous iteration (the kernel strides over its
-    // batches, so any grid is correct), at most what the GPU holds twice over
-    uint32_t g = 4608;
-    if (w.hint_small) g = std::min<uint32_t>(g, w.hint_small);
-    // Large iterations: the small-run waves go after the 129..384-row runs on the same stream —
-    // run concurrently they take the CUs whose whole LDS those workgroups need, and starve them.
-    static const uint32_t serial_min = [] {  // KLSH_SERIAL_MIN: positions from which to serialise
-      const char* e = getenv("KLSH_SERIAL_MIN");
-      return e ? (uint32_t)strtoul(e, nullptr, 10) : 0xFFFFFFFFu;
-    }();
-    k_merge_small<D><<<g, 64, 0, n >= serial_min ? f.lane(0) : f.lane(2)>>>(w, slots, dc, r, ctr);
-    return;
-  }
-  k_merge_group<64, D><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
-  k_merge_group<32, D><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
-  k_merge_group<16, D><<<grid(3, 4), 64, 0, f.lane(2)>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
-  k_merge_group<8, D><<<grid(2, 8), 64, 0, f.lane(2)>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
-  k_merge_group<4, D><<<grid(1, 16), 64, 0, f.lane(2)>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
-  k_merge_pair<D><<<pair_grid(n), 256, 0, f.lane(2)>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
+  launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
+  // every small-run class in one persistent launch (the kernel strides over its batches)
+  k_merge_small<D><<<4608, 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
 }
 
 template <int RB, int NT, int KC>
@@ -2093,15 +1840,13 @@ static void launch_big_wide(const MergeWork& w, int c, uint32_t* slots, const De
   }();
   (void)lds_ok;
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
-  uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
-  if (w.hint[c]) g = std::min(g, w.hint[c]);
-  k_merge_big_wide<RB, NT, KC><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist);
+  const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
+  k_merge_big_wide<RB, NT, KC><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist,
+                                                      w.rc);
 }
 
-static void launch_groups_wide(const Rows& r, const uint32_t* seg, uint32_t hi, int bucket_thr,
-                               uint32_t* slots, const Decider& dc, const MergeWork& w,
-                               Counters* ctr, uint32_t n, hipStream_t s) {
-  if (runs_via_scan()) k_classify<<<(n + 1023) / 1024, 1024, 0, s>>>(seg, hi, bucket_thr, w, ctr);
+static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc,
+                               const MergeWork& w, Counters* ctr, uint32_t n, hipStream_t s) {
   auto grid = [&](int c, uint32_t per_wave) {
     return (uint32_t)std::min<uint64_t>(2048, group_class_capacity(c, n) / per_wave + 1);
   };
@@ -2111,12 +1856,13 @@ static void launch_groups_wide(const Rows& r, const uint32_t* seg, uint32_t hi, 
   launch_big_wide<896, 256, 16>(w, 3, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, f.lane(1));
-  k_merge_group_wide<64><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<32><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<16><<<grid(3, 4), 64, 0, f.lane(2)>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<8><<<grid(2, 8), 64, 0, f.lane(2)>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<4><<<grid(1, 16), 64, 0, f.lane(2)>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist);
-  k_merge_group_wide<2><<<grid(0, 32), 64, 0, f.lane(2)>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist);
+  RunCounters* rc = w.rc;
+  k_merge_group_wide<64><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist, rc);
+  k_merge_group_wide<32><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist, rc);
+  k_merge_group_wide<16><<<grid(3, 4), 64, 0, f.lane(2)>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist, rc);
+  k_merge_group_wide<8><<<grid(2, 8), 64, 0, f.lane(2)>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist, rc);
+  k_merge_group_wide<4><<<grid(1, 16), 64, 0, f.lane(2)>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist, rc);
+  k_merge_group_wide<2><<<grid(0, 32), 64, 0, f.lane(2)>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist, rc);
 }
 
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
@@ -2124,16 +1870,13 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   if (hi <= lo) return;
   const uint32_t n = hi - lo;
   const Decider dc = make_decider(thr);
-  if (runs_via_scan())
-    device_scan(SrcHead{key, lo}, DstSegStart{w.seg, lo}, n, w.tile_sums, &ctr->n_seg, &ctr->err, s);
-  else
-    k_runs<<<(n + kRunTile - 1) / kRunTile, 256, 0, s>>>(key, lo, n, bucket_thr, w, ctr);
+  k_runs<<<(n + kRunTile - 1) / kRunTile, 256, 0, s>>>(key, lo, n, bucket_thr, w);
   switch (r.d) {
-    case 8: launch_groups<8>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
-    case 16: launch_groups<16>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
-    case 32: launch_groups<32>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
-    case 64: launch_groups<64>(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s); break;
-    default: launch_groups_wide(r, w.seg, hi, bucket_thr, slots, dc, w, ctr, n, s);
+    case 8: launch_groups<8>(r, slots, dc, w, ctr, n, s); break;
+    case 16: launch_groups<16>(r, slots, dc, w, ctr, n, s); break;
+    case 32: launch_groups<32>(r, slots, dc, w, ctr, n, s); break;
+    case 64: launch_groups<64>(r, slots, dc, w, ctr, n, s); break;
+    default: launch_groups_wide(r, slots, dc, w, ctr, n, s);
   }
 }
 

@@ -229,12 +229,14 @@ int launch_partition(const uint32_t* keys, const uint32_t* slots, uint32_t n, in
 }
 
 // ------------------------------------------------------------------------------- deltas -----
-// One thread per record word: consecutive lanes write consecutive words (and read one row).
+// One thread per record word, grid-strided (a launch stays below 2^32 work-items): consecutive
+// lanes write consecutive words (and read one row).
+constexpr uint32_t kDeltaGrid = 65536;
 __global__ __launch_bounds__(256) void k_delta_pack(Rows r, const uint32_t* __restrict__ ds,
                                                     uint32_t n, uint32_t* __restrict__ rec) {
   const uint32_t R = (uint32_t)delta_words(r.dp);
-  const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (t >= (uint64_t)n * R) return;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < (uint64_t)n * R;
+       t += (uint64_t)gridDim.x * 256u) {
   const uint32_t i = (uint32_t)(t / R), w = (uint32_t)(t % R);
   const uint32_t s = ds[i];
   uint32_t v;
@@ -247,19 +249,22 @@ __global__ __launch_bounds__(256) void k_delta_pack(Rows r, const uint32_t* __re
     default: v = __float_as_uint(r.x[(size_t)s * r.dp + (w - 5)]);
   }
   rec[t] = v;
+  }
 }
 
 void launch_delta_pack(const Rows& r, const uint32_t* delta_slots, uint32_t n, uint32_t* rec,
                        hipStream_t s) {
   const uint64_t total = (uint64_t)n * (uint64_t)delta_words(r.dp);
-  if (total) k_delta_pack<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(r, delta_slots, n, rec);
+  if (total)
+    k_delta_pack<<<(unsigned)std::min<uint64_t>((total + 255) / 256, kDeltaGrid), 256, 0, s>>>(
+        r, delta_slots, n, rec);
 }
 
 __global__ __launch_bounds__(256) void k_delta_apply(Rows r, const uint32_t* __restrict__ rec,
                                                      uint32_t n) {
   const uint32_t R = (uint32_t)delta_words(r.dp);
-  const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (t >= (uint64_t)n * R) return;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x; t < (uint64_t)n * R;
+       t += (uint64_t)gridDim.x * 256u) {
   const uint32_t i = (uint32_t)(t / R), w = (uint32_t)(t % R);
   const uint32_t s = rec[(uint64_t)i * R];
   const uint32_t v = rec[t];
@@ -271,11 +276,14 @@ __global__ __launch_bounds__(256) void k_delta_apply(Rows r, const uint32_t* __r
     case 4: r.nrm[s] = __uint_as_float(v); break;
     default: r.x[(size_t)s * r.dp + (w - 5)] = __uint_as_float(v);
   }
+  }
 }
 
 void launch_delta_apply(const Rows& r, const uint32_t* rec, uint32_t n, hipStream_t s) {
   const uint64_t total = (uint64_t)n * (uint64_t)delta_words(r.dp);
-  if (total) k_delta_apply<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(r, rec, n);
+  if (total)
+    k_delta_apply<<<(unsigned)std::min<uint64_t>((total + 255) / 256, kDeltaGrid), 256, 0, s>>>(
+        r, rec, n);
 }
 
 __global__ __launch_bounds__(256) void k_min_u32(uint32_t* __restrict__ a,

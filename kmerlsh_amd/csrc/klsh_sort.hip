@@ -1,0 +1,200 @@
+// Stable bucketing of one LSH iteration: merge_hashtable (reference function/cluster.cc:15-30)
+// walks the rows in canonical order and appends each to the bucket of its key; buckets are then
+// visited in ascending key order.  That is exactly a stable sort of (key, slot) by key, done here
+// as an LSD radix sort with B-bit digits (B = 8..10, so 23-bit keys take three passes and
+// 17..20-bit keys two).  Per pass, three launches:
+//
+//   k_sort_hist     per-tile digit counts, [digit][tile] (4096-key tiles)
+//   k_sort_dscan    one workgroup per digit: exclusive scan of its row over the tiles + the digit's
+//                   total (no look-back: every row is independent, digit bases come from the
+//                   totals, which each scatter workgroup scans itself)
+//   k_sort_scatter  ranks of the tile's keys among equal digits (wave ballots, in position order),
+//                   the tile ordered by digit in LDS, then written out in per-digit runs
+//
+// Tile layout: wave w of a workgroup owns the 1024 consecutive positions [w*1024, w*1024 + 1024)
+// of its tile, item j of lane l being position w*1024 + j*64 + l — every load and store
+// instruction is one contiguous 256-B segment, and a wave's running per-digit counts taken in item
+// order are ranks in position order (stability).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "klsh_device.cuh"
+
+namespace klsh {
+
+constexpr uint32_t kSortTile = 4096;  // keys per workgroup (4 waves x 16 items x 64 lanes)
+constexpr int kSortItems = 16;
+
+template <int B>
+__global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys, uint32_t n,
+                                                   int shift, uint32_t ntiles,
+                                                   uint32_t* __restrict__ hist) {
+  constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u;
+  __shared__ uint32_t c[RAD];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  for (uint32_t d = t; d < RAD; d += 256) c[d] = 0u;
+  const uint32_t base = blockIdx.x * kSortTile + wv * 1024u + lane;
+  uint32_t k[kSortItems];
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const uint32_t p = base + (uint32_t)j * 64u;
+    k[j] = p < n ? keys[p] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j)
+    if (base + (uint32_t)j * 64u < n) atomicAdd(&c[(k[j] >> shift) & MASK], 1u);
+  __syncthreads();
+  for (uint32_t d = t; d < RAD; d += 256) hist[(size_t)d * ntiles + blockIdx.x] = c[d];
+}
+
+// Workgroup d: hist[d][0..ntiles) -> its exclusive prefix over the tiles; dtot[d] = digit total.
+__global__ __launch_bounds__(256) void k_sort_dscan(uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                    uint32_t* __restrict__ dtot) {
+  uint32_t* row = hist + (size_t)blockIdx.x * ntiles;
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (ntiles + 255u) / 256u;
+  const uint32_t lo = min(ntiles, t * per), hi = min(ntiles, lo + per);
+  uint32_t acc = 0;
+  for (uint32_t i = lo; i < hi; ++i) acc += row[i];
+  uint32_t total;
+  uint32_t run = block_excl_scan_256(acc, &total);
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t v = row[i];
+    row[i] = run;
+    run += v;
+  }
+  if (t == 0) dtot[blockIdx.x] = total;
+}
+
+template <int B>
+__global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict__ kin,
+                                                      const uint32_t* __restrict__ vin,
+                                                      uint32_t* __restrict__ kout,
+                                                      uint32_t* __restrict__ vout, uint32_t n,
+                                                      int shift, uint32_t ntiles,
+                                                      const uint32_t* __restrict__ hist,
+                                                      const uint32_t* __restrict__ dtot) {
+  constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u, PER = RAD / 256u;
+  __shared__ uint32_t lk[kSortTile], lv[kSortTile];
+  __shared__ uint32_t wc[4][RAD];  // per-wave running digit counts, then their wave prefixes
+  __shared__ uint32_t ls[RAD];     // tile-local start of each digit
+  __shared__ uint32_t gb[RAD];     // output position of tile-local entry 0 of each digit
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t T0 = blockIdx.x * kSortTile;
+  const uint32_t base = T0 + wv * 1024u + lane;
+  for (uint32_t i = t; i < 4u * RAD; i += 256) (&wc[0][0])[i] = 0u;
+  uint32_t k[kSortItems], v[kSortItems];
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const uint32_t p = base + (uint32_t)j * 64u;
+    k[j] = p < n ? kin[p] : 0u;
+    v[j] = p < n ? vin[p] : 0u;
+  }
+  __syncthreads();
+  // rank of each item among the wave's earlier items with the same digit
+  const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  uint32_t lr[kSortItems];
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    const bool valid = base + (uint32_t)j * 64u < n;
+    const uint32_t dig = (k[j] >> shift) & MASK;
+    uint64_t match = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const bool bit = (dig >> b) & 1u;
+      const uint64_t mb = __ballot(bit);
+      match &= bit ? mb : ~mb;
+    }
+    const uint32_t old = wc[wv][dig];  // every lane reads before the group's leader writes
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (valid && (match & lt) == 0ull) wc[wv][dig] = old + (uint32_t)__popcll(match);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    lr[j] = old + (uint32_t)__popcll(match & lt);
+  }
+  __syncthreads();
+  // per digit: wave prefixes, tile totals -> local starts; digit totals -> global bases
+  uint32_t tot[PER], dt[PER];
+  uint32_t acc = 0, dacc = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t d = t * PER + q;
+    const uint32_t c0 = wc[0][d], c1 = wc[1][d], c2 = wc[2][d], c3 = wc[3][d];
+    wc[0][d] = 0u;
+    wc[1][d] = c0;
+    wc[2][d] = c0 + c1;
+    wc[3][d] = c0 + c1 + c2;
+    tot[q] = c0 + c1 + c2 + c3;
+    acc += tot[q];
+    dt[q] = dtot[d];
+    dacc += dt[q];
+  }
+  uint32_t total;
+  uint32_t lpre = block_excl_scan_256(acc, &total);
+  uint32_t dpre = block_excl_scan_256(dacc, &total);
+#pragma unroll
+  for (uint32_t q = 0; q < PER; ++q) {
+    const uint32_t d = t * PER + q;
+    ls[d] = lpre;
+    gb[d] = dpre + hist[(size_t)d * ntiles + blockIdx.x] - lpre;
+    lpre += tot[q];
+    dpre += dt[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSortItems; ++j) {
+    if (base + (uint32_t)j * 64u < n) {
+      const uint32_t dig = (k[j] >> shift) & MASK;
+      const uint32_t pos = ls[dig] + wc[wv][dig] + lr[j];
+      lk[pos] = k[j];
+      lv[pos] = v[j];
+    }
+  }
+  __syncthreads();
+  const uint32_t m = min(kSortTile, n - T0);
+  for (uint32_t e = t; e < m; e += 256) {
+    const uint32_t kk = lk[e];
+    const uint32_t o = gb[(kk >> shift) & MASK] + e;
+    kout[o] = kk;
+    vout[o] = lv[e];
+  }
+}
+
+uint64_t sort_ws_words(uint64_t slots) {
+  // [digit][tile] counts for up to 2^10 digits, then the digit totals
+  return 1024ull * ((slots + kSortTile - 1) / kSortTile) + 1024 + 64;
+}
+
+template <int B>
+static void sort_pass(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo,
+                      uint32_t n, int shift, uint32_t* ws, hipStream_t s) {
+  const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
+  uint32_t* hist = ws;
+  uint32_t* dtot = ws + (size_t)(1u << B) * ntiles;
+  k_sort_hist<B><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, hist);
+  k_sort_dscan<<<1u << B, 256, 0, s>>>(hist, ntiles, dtot);
+  k_sort_scatter<B><<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, hist, dtot);
+}
+
+void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
+                uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s) {
+  uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
+  if (n > 1 && bits > 0) {
+    // P passes of B-bit digits: 1..10 bits one pass, 11..20 two, 21..30 three, 31..32 four
+    const int P = (bits + 9) / 10;
+    const int B = std::max(8, (bits + P - 1) / P);
+    for (int p = 0; p < P; ++p) {
+      const int shift = p * B;
+      if (B == 8) sort_pass<8>(ki, vi, ko, vo, n, shift, ws, s);
+      else if (B == 9) sort_pass<9>(ki, vi, ko, vo, n, shift, ws, s);
+      else sort_pass<10>(ki, vi, ko, vo, n, shift, ws, s);
+      std::swap(ki, ko);
+      std::swap(vi, vo);
+    }
+  }
+  *out_k = ki;
+  *out_v = vi;
+}
+
+}  // namespace klsh

@@ -36,10 +36,9 @@ def test_target_is_gfx950(kernels):
 
 def test_projection_has_no_fused_multiply_add(kernels):
     proj = {k: v for k, v in kernels.items() if "k_project" in k}
-    # d = 8, 16, 32, 64: scalar (direct, staged) and packed (4 chains, 8 chains with 1 or 2 rows
-    # per lane); packed wide-row kernels (1 and 4 rows per lane); the generic kernel; the
-    # matrix-core kernels (d = 16, 32, 64; wide rows + their exact fix-up kernel)
-    assert len(proj) == 28
+    # d = 8, 16, 32, 64: packed (8 chains, 1 row per lane); the packed wide-row kernel; the generic
+    # kernel; the matrix-core kernels (d = 16, 32, 64; wide rows + their exact fix-up kernel)
+    assert len(proj) == 11
     for name, body in proj.items():
         bad = [ln.strip() for ln in body.splitlines() if FMA.match(ln)]
         assert not bad, (name, bad[:5])

@@ -1,5 +1,4 @@
-// Microbenchmark of the bucket sort and the scan (A/B of the variants selected by KLSH_SORT /
-// KLSH_SCAN).  Build: make -C kmerlsh_amd/csrc ubench; run: tools/ubench_sort N BITS REPS.
+// Microbenchmark of the bucket sort (klsh_sort.hip) and the device scan.  Build: make -C kmerlsh_amd/csrc ubench; run: tools/ubench_sort N BITS REPS.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -59,7 +58,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpyAsync(k0, kk, 4ull * n, hipMemcpyDeviceToDevice, s));
     CK(hipMemcpyAsync(v0, vv, 4ull * n, hipMemcpyDeviceToDevice, s));
     CK(hipEventRecord(a, s));
-    klsh::radix_sort(k0, v0, k1, v1, n, bits, ws, ts, ctr, &ok, &ov, s);
+    klsh::radix_sort(k0, v0, k1, v1, n, bits, ws, &ok, &ov, s);
     CK(hipEventRecord(b, s));
     CK(hipStreamSynchronize(s));
     float ms;
@@ -93,9 +92,8 @@ int main(int argc, char** argv) {
   }
   klsh::Counters hc;
   CK(hipMemcpy(&hc, ctr, sizeof(hc), hipMemcpyDeviceToHost));
-  printf("n=%u bits=%d sort=%s %.1f us  scan=%s %.1f us  total=%u (want %u) err=%u  [KLSH_SORT=%s KLSH_SCAN=%s]\n",
+  printf("n=%u bits=%d sort=%s %.1f us  scan=%s %.1f us  total=%u (want %u) err=%u\n",
          n, bits, sort_ok ? "ok" : "BAD", 1e3 * sort_ms / reps, scan_ok ? "ok" : "BAD",
-         1e3 * scan_ms / reps, hc.total, run, hc.err, getenv("KLSH_SORT") ? getenv("KLSH_SORT") : "-",
-         getenv("KLSH_SCAN") ? getenv("KLSH_SCAN") : "-");
+         1e3 * scan_ms / reps, hc.total, run, hc.err);
   return sort_ok && scan_ok && hc.err == 0 ? 0 : 1;
 }
