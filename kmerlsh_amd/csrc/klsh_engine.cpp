@@ -236,7 +236,7 @@ struct klsh_ctx {
   void release_state() {
     dfree(rows.x); dfree(rows.nrm); dfree(rows.cnt); dfree(rows.head); dfree(rows.tail);
     dfree(rows.nxt); dfree(order); dfree(alt); dfree(keys); dfree(keys2); dfree(nk1);
-    dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.over);
+    dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.over); dfree(mw.run_ws);
     dfree(mw.huge);
     dfree(pw.fix);
     dfree(pw.ws);
@@ -304,7 +304,7 @@ struct klsh_ctx {
         (e = dalloc(&nv2, s)) ||
         (e = dalloc(&hist, klsh::sort_ws_words(s))) ||
         (e = dalloc(&tile_sums, klsh::scan_ws_words(s))) ||
-        (e = dalloc(&mw.over, s + 64)) ||
+        (e = dalloc(&mw.over, s + 64)) || (e = dalloc(&mw.run_ws, klsh::run_ws_words(s))) ||
         (e = dalloc(&pw.fix, s)) || (e = dalloc(&pw.ws, 64)) ||
         (e = dalloc(&mw.big[0], s / 65 + 64)) || (e = dalloc(&mw.big[1], s / 129 + 64)) ||
         (e = dalloc(&mw.big[2], s / 193 + 64)) || (e = dalloc(&mw.big[3], s / 385 + 64)) ||

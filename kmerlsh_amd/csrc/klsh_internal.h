@@ -49,6 +49,10 @@ struct RunCounters {
   CountLine n_seg, n_cls[kGroupClasses], n_big[kBigClasses], n_huge, n_over;
 };
 
+// Run-finding workspace (u32 words) for `slots` positions: 13 counts + a tail end + a 4096-bit
+// head bitmap per 4096-position tile.
+inline uint64_t run_ws_words(uint64_t slots) { return (slots / 4096 + 2) * (13 + 1 + 128) + 64; }
+
 // Device-side per-iteration counters (zeroed by the host before each iteration).
 struct Counters {
   uint32_t n_seg;                  // bucket runs (k_runs)
@@ -70,6 +74,7 @@ struct MergeWork {
   uint2* over;                     // (start, length) of oversize runs
   uint32_t* tile_sums;
   RunCounters* rc;                 // the run counts of this iteration (device)
+  uint32_t* run_ws;                // run finding: per-tile list counts, head bitmaps (run_ws_words)
   // Sharded loop only (nullptr otherwise): every survivor a merge rewrote is appended to dlist
   // (ctr->n_delta entries, any order, each slot once); mark[slot] == stamp dedupes the kernels
   // that merge in place (stamp: unique per iteration, never reused by a context).

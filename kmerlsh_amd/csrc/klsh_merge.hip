@@ -165,11 +165,35 @@ __device__ __forceinline__ int size_class(uint32_t b) {  // G = 2 << class lanes
   return b <= 2 ? 0 : b <= 4 ? 1 : b <= 8 ? 2 : b <= 16 ? 3 : b <= 32 ? 4 : 5;
 }
 
+// Pre-screen of one pair from an approximate dot product g (a Gram tile, or short chains) within
+// kGramMargin * |a||b| of the reference's sequential one: 1 = merge, 0 = no merge, 2 = too close
+// to call (or den outside the fast range): the exact sequential dot decides.
+__device__ __forceinline__ uint32_t prescreen(const Decider& dc, float g, float den) {
+  if (den >= 0x1p-60f && den <= 0x1p60f) {
+    const float q = g * __builtin_amdgcn_rcpf(den);
+    if (q >= dc.g_hi) return 1u;
+    if (q <= dc.g_lo) return 0u;
+  }
+  return 2u;
+}
+
 // --------------------------------------------------------------------- G-lane groups -----
-// The wave handles n runs listed in LDS (ents), 64/G at a time.  Lane g of a group is position
-// g of its run and owns row id g: row in registers x[] and at LDS row `lane`.
-// One batch: run (p, b) of lane's group, lane's slot already loaded (the caller pipelines those
-// loads one batch ahead, so only the row gather is exposed here).
+// One batch: 64/G runs of one size class, G lanes per run; lane g of a group is position g of its
+// run and holds that position's row (registers, and LDS row `lane` for its partners).  The lane's
+// slot is already loaded (the caller pipelines it one batch ahead).
+//
+// 1. Every pairwise decision of the run, each unordered pair once (lane g pairs with the rows
+//    k = 1 .. b/2 positions after it, cyclically; decide(a, c) == decide(c, a): the same products
+//    in the same order and the same sqrt product, so the partner receives the bit).  The result is
+//    the symmetric decision matrix, one row of position bits per lane.
+// 2. The walk, kept in POSITION space: lane q holds the bits of the row at position q against the
+//    rows at every position (P), that row's id, slot, metadata and data.  The next merge is the
+//    first lane q >= i whose P has a bit below q (one ballot); its first match j is the lowest lane
+//    p < i whose bit i is set (the matrix is symmetric: one more ballot).  A merge rewrites the row
+//    at j (consensus, split over the group's lanes, in LDS), moves the last position's row and
+//    state to lane i (swap-remove), remaps bit `last` to bit i everywhere, and re-decides bit j
+//    for the positions still to be visited — through the certified short-chain screen, exact
+//    chains only for close calls — whose ballot is the new row's P.
 template <int G, int D>
 __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
                                             uint32_t* slots, const Decider& dc, const Rows& r,
@@ -182,33 +206,35 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
   float* myrow = lds + lane * ST;
   [[maybe_unused]] const uint64_t sp0 = WPROF_CLK();
   [[maybe_unused]] uint64_t sp1 = 0, sp2 = 0, sp3 = 0;
-  {
-    const bool valid = g < b;
-    // member count / list ends: only a merge needs them, and most batches have none — they are
-    // loaded after the pairwise decisions, by waves that found a matching pair (saves three
-    // random 4-B reads per row, as much traffic as the row itself)
-    uint32_t cnt = 0u, hd = 0u, tl = 0u;
-    stage_rows<D>(r.x, r.dp, slot, valid, lds);  // row of lane l -> LDS row l, coalesced
-    wave_lds_fence();
-    float x[D];
-    load_row<D>(myrow, x);
-    // the row's norm: recomputed from the row (the same sequential chain that made the cached
-    // value, distance.cc:33-34, so the same bits) instead of a random 4-B read of r.nrm
-    float nrm = 0.0f;
+  const bool valid = g < b;
+  // the lane's own row straight from memory (no cross-lane address shuffles), then to LDS for its
+  // partners
+  float x[D];
+  if (valid) {
+    load_row<D>(r.x + (size_t)slot * r.dp, x);
+  } else {
 #pragma unroll
-    for (int k = 0; k < D; ++k) nrm = nrm + x[k] * x[k];
-    if (!valid) nrm = 0.0f;
-    float sq = __builtin_sqrtf(nrm);  // this row's sqrtf(|x|^2), distance.cc:37
-    const uint32_t bmax = wave_max(b);
+    for (int k = 0; k < D; ++k) x[k] = 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < D; k += 4)
+    *reinterpret_cast<float4*>(myrow + k) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
+  wave_lds_fence();
+  // the row's norm: recomputed from the row (the same sequential chain that made the cached
+  // value, distance.cc:33-34, so the same bits) instead of a random 4-B read of r.nrm
+  float nrm = 0.0f;
+#pragma unroll
+  for (int k = 0; k < D; ++k) nrm = nrm + x[k] * x[k];
+  float sq = __builtin_sqrtf(nrm);  // this row's sqrtf(|x|^2), distance.cc:37
+  const uint32_t bmax = wave_max(b);
 #ifdef KLSH_MERGE_PROF
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    sp1 = WPROF_CLK();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  sp1 = WPROF_CLK();
 #endif
 
-    // 1. every pairwise decision of the run, each unordered pair once: lane g pairs with the
-    //    rows k = 1 .. b/2 positions after it, cyclically.  decide(a, c) == decide(c, a) (same
-    //    products in the same order, the same sqrt product), so the partner receives the bit.
-    uint64_t full = 0ull;
+  // 1. the pairwise decisions
+  uint64_t P = 0ull;  // group-local position bits
+  {
     const uint32_t half = b / 2;
     auto partner = [&](uint32_t k) {  // (g + k) mod b, for k <= b
       const uint32_t j = g + k;
@@ -218,8 +244,8 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
       const uint32_t src = g >= k ? g - k : g + b - k;  // lane holding decide(src, g)
       const uint32_t in = (uint32_t)__shfl((int)bit, (int)(gbase + (src & (G - 1))), 64);
       if (valid && k <= half) {
-        full |= (uint64_t)bit << partner(k);
-        full |= (uint64_t)in << src;
+        P |= (uint64_t)bit << partner(k);
+        P |= (uint64_t)in << src;
       }
     };
     for (uint32_t k = 1; k <= bmax / 2; k += 2) {  // two partners per step: independent chains
@@ -235,97 +261,146 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
       share(k, h0);
       share(k + 1, h1);
     }
-
-    if (__ballot(valid && full != 0ull)) {  // some run of the wave merges
-      if (valid) {
-        cnt = r.cnt[slot];
-        hd = r.head[slot];
-        tl = r.tail[slot];
-      }
-    }
+  }
 #ifdef KLSH_MERGE_PROF
-    sp2 = WPROF_CLK();
+  sp2 = WPROF_CLK();
 #endif
-    // 2. replay the walk on the bits.  Positions that find no candidate below them change
-    //    nothing, so each round jumps straight to the first position q >= i whose row matches
-    //    some row at a position below q (exclusive prefix-OR of row bits over positions).
-    uint32_t rowid = g;  // row id at my position
-    uint32_t mypos = g;  // position of my row
-    bool alive = valid, dirty = false;
-    uint32_t i = 1, size = b;  // uniform within the group
+
+  // 2. the walk.  Per position lane: row id, slot, member count / list ends (loaded only by waves
+  //    with a matching pair: three random 4-B reads per row, as much traffic as the row itself),
+  //    the row's sqrt-norm, the row (x), dirty = rewritten by a merge.
+  uint32_t size = b;
+  uint32_t nmerged = 0;
+  bool dirty = false;
+  if (__ballot(valid && P != 0ull)) {
+    uint32_t rid = g, cnt = 0u, hd = 0u, tl = 0u;
+    if (valid) {
+      cnt = r.cnt[slot];
+      hd = r.head[slot];
+      tl = r.tail[slot];
+    }
+    uint32_t i = 1;  // group-uniform
     while (true) {
-      const uint64_t mybit = g < size ? (1ull << rowid) : 0ull;
-      uint64_t incl = mybit;
-#pragma unroll
-      for (uint32_t o = 1; o < (uint32_t)G; o <<= 1) {
-        const uint64_t y = shfl64(incl, lane >= o ? lane - o : lane);
-        if (g >= o) incl |= y;
-      }
-      const uint64_t frow = shfl64(full, gbase + rowid);  // decisions of the row at my position
-      const bool hit = g >= i && g < size && (frow & (incl & ~mybit)) != 0ull;
+      const uint64_t below = g ? (~0ull >> (64u - g)) : 0ull;
+      const bool hit = g >= i && g < size && (P & below) != 0ull;
       const uint64_t m = __ballot(hit) & gmask;
       if (__ballot(m != 0ull) == 0ull) break;  // every group of the wave is done
-      if (m != 0ull) {
-        i = (uint32_t)(__ffsll((unsigned long long)m) - 1) - gbase;  // the reference's i
-        const uint32_t rr = shfl32(rowid, gbase + i);
-        const uint64_t fr = shfl64(frow, gbase + i);
-        const uint64_t mj = __ballot(g < i && ((fr >> rowid) & 1ull)) & gmask;
-        const uint32_t jpos = (uint32_t)(__ffsll((unsigned long long)mj) - 1) - gbase;
-        const uint32_t c = shfl32(rowid, gbase + jpos);  // first matching candidate (row j)
-        const uint32_t ca = shfl32(cnt, gbase + rr), cb = shfl32(cnt, gbase + c);
-        const uint32_t hr = shfl32(hd, gbase + rr), tr = shfl32(tl, gbase + rr);
-        const uint32_t hc = shfl32(hd, gbase + c);
-        const uint32_t slot_c = shfl32(slot, gbase + c);
-        const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
-        const float* rowr = lds + (gbase + rr) * ST;
-        float* rowc = lds + (gbase + c) * ST;
-        (void)slot_c;
-        for (int k = (int)g; k < D; k += G)  // consensus, split over the group's lanes (LDS only:
-          rowc[k] = consensus(rowr[k], fa, rowc[k], fb, fn);  // rewritten rows go out at the end)
-        wave_lds_fence();
-        // one pass: lane c (the new row c, reloaded) gets its exact sequential norm
-        // (distance.cc:33-34), every other lane the dot product of its row with row c
-        if (g == c) load_row<D>(rowc, x);
-        const float dot = dot_reg_lds<D>(x, rowc);
-        if (g == c) {
-          nrm = dot;
-          sq = __builtin_sqrtf(dot);
-          cnt = ca + cb;
-          hd = hr;
+      const bool active = m != 0ull;
+      uint32_t j = 0, last = 0;
+      if (active) {
+        i = (uint32_t)__builtin_ctzll(m >> gbase);
+        j = (uint32_t)__builtin_ctzll((__ballot(g < i && ((P >> i) & 1ull)) & gmask) >> gbase);
+        last = size - 1;
+      }
+      // the rows at positions i (current), j (candidate), last (moves to i)
+      const uint32_t li = gbase + (i & (G - 1)), lj = gbase + (j & (G - 1));
+      const uint32_t ll = gbase + (last & (G - 1));
+      const uint32_t ri = shfl32(rid, li), rj = shfl32(rid, lj);
+      const uint32_t ci = shfl32(cnt, li), cj = shfl32(cnt, lj);
+      const uint32_t hi_ = shfl32(hd, li), ti = shfl32(tl, li), hj = shfl32(hd, lj);
+      const uint32_t m_rid = shfl32(rid, ll), m_slot = shfl32(slot, ll), m_cnt = shfl32(cnt, ll);
+      const uint32_t m_hd = shfl32(hd, ll), m_tl = shfl32(tl, ll);
+      const float m_sq = shflf(sq, ll);
+      const uint64_t m_P = shfl64(P, ll);
+      if (active) {
+        // consensus (funcAB.cc:65), current row first, split over the group's lanes, in place
+        const float fa = (float)(int)ci, fb = (float)(int)cj, fn = (float)(int)(ci + cj);
+        const float* rowr = lds + (gbase + ri) * ST;
+        float* rowc = lds + (gbase + rj) * ST;
+        for (int k = (int)g; k < D; k += G) rowc[k] = consensus(rowr[k], fa, rowc[k], fb, fn);
+        if (g == j) {
+          r.nxt[ti] = hj;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
+          cnt = ci + cj;
+          hd = hi_;
           dirty = true;
         }
-        if (g == rr) alive = false;
-        if (g == 0) r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
-        const uint32_t last = shfl32(rowid, gbase + size - 1);  // swap-remove
-        if (g == i) rowid = last;
-        if (g == last) mypos = i;
-        --size;
-        const float sc = shflf(sq, gbase + c);
-        if (alive && mypos >= i && mypos < size) {  // rows still to be visited vs the new row c
-          full = decide(dc, dot, sq * sc) ? (full | (1ull << c)) : (full & ~(1ull << c));
+        if (g == i) r.cnt[slot] = 0u;  // the current row is gone
+        // swap-remove: the last position's row and state move to position i
+        if (g == i && i != last) {
+          rid = m_rid;
+          slot = m_slot;
+          cnt = m_cnt;
+          hd = m_hd;
+          tl = m_tl;
+          sq = m_sq;
+          P = m_P;
         }
+        if (i != last) {
+          const uint64_t bl = (P >> last) & 1ull;
+          P = (P & ~((1ull << i) | (1ull << last))) | (bl << i);
+        }
+        --size;
+        ++nmerged;
       }
-    }
-
-#ifdef KLSH_MERGE_PROF
-    sp3 = WPROF_CLK();
-#endif
-    // 3. write back: survivors in position order, kInvalid after; changed rows and metadata
-    const uint32_t pos_slot = shfl32(slot, gbase + rowid);
-    if (valid && size < b) slots[p + g] = g < size ? pos_slot : kInvalid;  // runs that merged
-    if (valid && alive && dirty) {
-      float* xo = r.x + (size_t)slot * r.dp;
+      wave_lds_fence();
+      const bool need = active && g >= i && g < size;
+      if (active && g == i && i < size) load_row<D>(lds + (gbase + rid) * ST, x);
+      // decisions of the positions still to be visited against the new row at j (read from LDS
+      // 16 B at a time: the chains need no copy of it in registers)
+      const float* cr = lds + (gbase + rj) * ST;
+      float n4[4] = {0.0f, 0.0f, 0.0f, 0.0f}, d4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int k = 0; k < D; k += 4)
-        *reinterpret_cast<float4*>(xo + k) = *reinterpret_cast<const float4*>(myrow + k);
-      r.nrm[slot] = nrm;
+      for (int k = 0; k < D; k += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(cr + k);
+        n4[0] = n4[0] + v.x * v.x;
+        n4[1] = n4[1] + v.y * v.y;
+        n4[2] = n4[2] + v.z * v.z;
+        n4[3] = n4[3] + v.w * v.w;
+        d4[0] = d4[0] + x[k] * v.x;
+        d4[1] = d4[1] + x[k + 1] * v.y;
+        d4[2] = d4[2] + x[k + 2] * v.z;
+        d4[3] = d4[3] + x[k + 3] * v.w;
+      }
+      uint32_t dn = 0u;
+      if (need) {
+        const float sc_a = __builtin_sqrtf((n4[0] + n4[1]) + (n4[2] + n4[3]));
+        dn = dc.fast ? prescreen(dc, (d4[0] + d4[1]) + (d4[2] + d4[3]), sq * sc_a) : 2u;
+      }
+      if (__ballot(dn == 2u)) {  // rare: the reference's sequential chains settle the close calls
+        float nn = 0.0f, dot = 0.0f;
+#pragma unroll
+        for (int k = 0; k < D; k += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(cr + k);
+          nn = nn + v.x * v.x;
+          nn = nn + v.y * v.y;
+          nn = nn + v.z * v.z;
+          nn = nn + v.w * v.w;
+          dot = dot + x[k] * v.x;
+          dot = dot + x[k + 1] * v.y;
+          dot = dot + x[k + 2] * v.z;
+          dot = dot + x[k + 3] * v.w;
+        }
+        if (dn == 2u) dn = decide(dc, dot, sq * __builtin_sqrtf(nn)) ? 1u : 0u;
+      }
+      const uint64_t dm = (__ballot(need && dn == 1u) & gmask) >> gbase;
+      if (need) P = dn ? (P | (1ull << j)) : (P & ~(1ull << j));
+      if (active && g == j) P = dm;  // the new row against the positions still to be visited
+    }
+    // write back: survivors in position order, kInvalid after; rewritten rows and metadata
+    if (valid && size < b) slots[p + g] = g < size ? slot : kInvalid;
+    if (valid && dirty) {  // a rewritten row sits at a position below every merge after it
+      const float* src = lds + (gbase + rid) * ST;
+      float* xo = r.x + (size_t)slot * r.dp;
+      float nv = 0.0f;  // its exact sequential norm (distance.cc:33-34)
+#pragma unroll
+      for (int k = 0; k < D; k += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src + k);
+        nv = nv + v.x * v.x;
+        nv = nv + v.y * v.y;
+        nv = nv + v.z * v.z;
+        nv = nv + v.w * v.w;
+        *reinterpret_cast<float4*>(xo + k) = v;
+      }
+      r.nrm[slot] = nv;
       r.cnt[slot] = cnt;
       r.head[slot] = hd;
     }
-    if (dlist) append_slot(valid && alive && dirty, slot, dlist, &ctr->n_delta);
-    if (valid && !alive) r.cnt[slot] = 0u;
-    wave_lds_fence();
   }
+#ifdef KLSH_MERGE_PROF
+  sp3 = WPROF_CLK();
+#endif
+  if (dlist) append_slot(valid && dirty, slot, dlist, &ctr->n_delta);
+  wave_lds_fence();
 #ifdef KLSH_MERGE_PROF
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) {
@@ -338,6 +413,7 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
     atomicAdd(&g_sprof[c][4], sp4 - sp3);
   }
 #endif
+  (void)nmerged;
 }
 
 // ------------------------------------------------- all small-run classes in one launch -----
@@ -480,106 +556,168 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
 }
 
 template <int D>
-__global__ __launch_bounds__(64) void k_merge_small(MergeWork w, uint32_t* __restrict__ slots,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_merge_small(
+    MergeWork w, uint32_t* __restrict__ slots,
                                                     Decider dc, Rows r, Counters* ctr) {
   __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
   small_loop<D>(w, slots, dc, r, ctr, lds, blockIdx.x, gridDim.x);
 }
 
-// Runs of equal keys found and listed by size class in one pass: a tile of 16384 positions is
-// read coalesced (position k*256 + t by thread t), head flags become a 16384-bit LDS bitmap (wave
-// ballots), each head finds its run's end as the next set bit (the last run of the tile looks past
-// the tile end, one wave, 64 keys per step).  Runs are counted per list in LDS, each list's range
-// is reserved with ONE global add per workgroup (every counter on a 128-B line of its own:
-// RunCounters), and the entries are written in a second sweep over the bitmap.  Entries within a
-// list are in no particular order; every merge result is positional.
-constexpr int kRunTile = 16384;
+// Runs of equal keys, listed by size class, in three launches and no contended atomics:
+//   k_runs_count  a tile of 4096 positions is read coalesced (position k*256 + t by thread t), its
+//                 head flags become a 4096-bit bitmap (wave ballots, kept in global memory with the
+//                 first head past the tile end), each head finds its run's end as the next set bit
+//                 and its list (size class, big class, huge, oversize); per-list counts per tile
+//   k_runs_scan   one workgroup per list: exclusive scan of its counts over the tiles, the total
+//                 into the list's counter
+//   k_runs_write  every head again from the stored bitmap, its entry at the tile's base + a rank
+// (one global add per list per tile — the single-kernel version — serialised ~2300 adds per counter
+// at C2 size, 80-100 us).  Entries within a list are in no particular order; every merge result is
+// positional.
+constexpr uint32_t kRunTile = 4096;
 constexpr int kRunLists = kGroupClasses + kBigClasses + 2;  // small classes, big classes, huge, over
-__global__ __launch_bounds__(256) void k_runs(const uint32_t* __restrict__ key, uint32_t lo,
-                                              uint32_t n, int bucket_thr, MergeWork w) {
-  __shared__ uint64_t hb[kRunTile / 64];  // head bitmap of the tile, word = 64 positions
-  __shared__ uint32_t lcnt[kRunLists + 1], lbase[kRunLists], lfill[kRunLists];
-  __shared__ uint32_t s_tail_end;  // first head at or after the tile end (or n)
+constexpr int kRunRows = kRunLists + 1;                      // + the head count (n_seg)
+
+__device__ __forceinline__ uint32_t* run_counter(RunCounters* rc, int l) {
+  return l < kGroupClasses ? &rc->n_cls[l].v
+         : l < kGroupClasses + kBigClasses ? &rc->n_big[l - kGroupClasses].v
+         : l == kRunLists - 2 ? &rc->n_huge.v
+         : l == kRunLists - 1 ? &rc->n_over.v : &rc->n_seg.v;
+}
+
+// The run starting at tile-local position q (a head of bitmap hb): its length and list (-1: one row).
+__device__ __forceinline__ int run_list(const uint64_t* hb, uint32_t T0, uint32_t tail_end,
+                                        uint32_t q, int bucket_thr, uint32_t& b) {
+  uint32_t wi = q >> 6;
+  uint64_t m = hb[wi] & ~((2ull << (q & 63u)) - 1ull);  // heads after q in its word
+  while (!m && ++wi < kRunTile / 64) m = hb[wi];
+  const uint32_t next = m ? T0 + wi * 64u + (uint32_t)__builtin_ctzll(m) : tail_end;
+  b = next - (T0 + q);
+  if (bucket_thr >= 0 && b > (uint32_t)bucket_thr) return kRunLists - 1;  // cluster.cc:286
+  if (b > 64u) {
+    if (b > (uint32_t)kBigRows[kBigClasses - 1]) return kRunLists - 2;
+    int c = 0;
+    while (b > (uint32_t)kBigRows[c]) ++c;
+    return kGroupClasses + c;
+  }
+  return b >= 2 ? size_class(b) : -1;
+}
+
+__global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__ key, uint32_t lo,
+                                                    uint32_t n, int bucket_thr, uint32_t ntiles,
+                                                    uint64_t* __restrict__ hbits,
+                                                    uint32_t* __restrict__ tail_ends,
+                                                    uint32_t* __restrict__ counts) {
+  __shared__ uint64_t hb[kRunTile / 64];
+  __shared__ uint32_t lcnt[kRunRows];
+  __shared__ uint32_t s_tail_end;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t T0 = blockIdx.x * (uint32_t)kRunTile;
-  if (t <= (uint32_t)kRunLists) lcnt[t] = 0u;
-  if (t < (uint32_t)kRunLists) lfill[t] = 0u;
+  const uint32_t T0 = blockIdx.x * kRunTile;
+  if (t < (uint32_t)kRunRows) lcnt[t] = 0u;
   const uint32_t* kp = key + lo;
-  for (int k0 = 0; k0 < kRunTile / 256; k0 += 16) {
-    uint32_t a[16], b[16];
+  uint32_t a[16], pv[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t i = T0 + (uint32_t)(k0 + k) * 256u + t;
-      a[k] = i < n ? kp[i] : 0u;
-      b[k] = (i < n && i > 0) ? kp[i - 1] : 0u;
-    }
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t i = T0 + (uint32_t)k * 256u + t;
+    a[k] = i < n ? kp[i] : 0u;
+    pv[k] = (i < n && i > 0) ? kp[i - 1] : 0u;
+  }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t i = T0 + (uint32_t)(k0 + k) * 256u + t;
-      const uint64_t m = __ballot(i < n && (i == 0 || a[k] != b[k]));
-      if (lane == 0) hb[(k0 + k) * 4 + wv] = m;
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t i = T0 + (uint32_t)k * 256u + t;
+    const uint64_t m = __ballot(i < n && (i == 0 || a[k] != pv[k]));
+    if (lane == 0) {
+      hb[k * 4 + wv] = m;
+      hbits[(size_t)blockIdx.x * (kRunTile / 64) + k * 4 + wv] = m;
     }
   }
   if (wv == 0) {  // the end of the tile's last run: the first head at or after T0 + kRunTile
-    uint32_t j = T0 + (uint32_t)kRunTile, end = n;
+    uint32_t j = T0 + kRunTile, end = n;
     while (j < n) {
       const uint32_t q = j + lane;
-      const bool h = q < n && kp[q] != kp[q - 1];
-      const uint64_t m = __ballot(h);
+      const uint64_t m = __ballot(q < n && kp[q] != kp[q - 1]);
       if (m) {
         end = j + (uint32_t)__builtin_ctzll(m);
         break;
       }
       j += 64u;
     }
-    if (lane == 0) s_tail_end = min(end, n);
+    if (lane == 0) {
+      s_tail_end = min(end, n);
+      tail_ends[blockIdx.x] = min(end, n);
+    }
   }
   __syncthreads();
   const uint32_t tail_end = s_tail_end;
-  // the run starting at tile position q (a head): its length and list (-1: a single row)
-  auto run_at = [&](uint32_t q, uint32_t& b) -> int {
-    uint32_t wi = q >> 6;
-    uint64_t m = hb[wi] & ~((2ull << (q & 63u)) - 1ull);  // heads after q in its word
-    while (!m && ++wi < (uint32_t)(kRunTile / 64)) m = hb[wi];
-    const uint32_t next = m ? T0 + wi * 64u + (uint32_t)__builtin_ctzll(m) : tail_end;
-    b = next - (T0 + q);
-    if (bucket_thr >= 0 && b > (uint32_t)bucket_thr) return kRunLists - 1;  // cluster.cc:286
-    if (b > 64u) {
-      if (b > (uint32_t)kBigRows[kBigClasses - 1]) return kRunLists - 2;
-      int c = 0;
-      while (b > (uint32_t)kBigRows[c]) ++c;
-      return kGroupClasses + c;
-    }
-    return b >= 2 ? size_class(b) : -1;
-  };
+  const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   uint32_t heads = 0;
-  for (int k = 0; k < kRunTile / 256; ++k) {
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
     const uint32_t q = (uint32_t)k * 256u + t;
+    int l = -1;
     if ((hb[q >> 6] >> (q & 63u)) & 1ull) {
       uint32_t b;
-      const int l = run_at(q, b);
+      l = run_list(hb, T0, tail_end, q, bucket_thr, b);
       ++heads;
-      if (l >= 0) atomicAdd(&lcnt[l], 1u);
     }
+    // lanes with the same list: one LDS add by the lowest of them
+    const uint32_t id = (uint32_t)(l + 1);  // 0 = no entry
+    uint64_t match = ~0ull;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+      const uint64_t mb = __ballot((id >> bit) & 1u);
+      match &= ((id >> bit) & 1u) ? mb : ~mb;
+    }
+    if (l >= 0 && (match & lt) == 0ull) atomicAdd(&lcnt[l], (uint32_t)__popcll(match));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) heads += __shfl_xor(heads, o, 64);
   if (lane == 0 && heads) atomicAdd(&lcnt[kRunLists], heads);
   __syncthreads();
-  auto counter = [&](int l) -> uint32_t* {
-    RunCounters* rc = w.rc;
-    return l < kGroupClasses ? &rc->n_cls[l].v
-           : l < kGroupClasses + kBigClasses ? &rc->n_big[l - kGroupClasses].v
-           : l == kRunLists - 2 ? &rc->n_huge.v : &rc->n_over.v;
-  };
-  if (t < (uint32_t)kRunLists && lcnt[t]) lbase[t] = atomicAdd(counter((int)t), lcnt[t]);
-  if (t == (uint32_t)kRunLists && lcnt[t]) atomicAdd(&w.rc->n_seg.v, lcnt[t]);
+  if (t < (uint32_t)kRunRows) counts[(size_t)t * ntiles + blockIdx.x] = lcnt[t];
+}
+
+// Workgroup l: counts[l][0..ntiles) -> exclusive prefix over the tiles; the total -> list l's counter.
+__global__ __launch_bounds__(256) void k_runs_scan(uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                   RunCounters* rc) {
+  uint32_t* row = counts + (size_t)blockIdx.x * ntiles;
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (ntiles + 255u) / 256u;
+  const uint32_t a = min(ntiles, t * per), e = min(ntiles, a + per);
+  uint32_t acc = 0;
+  for (uint32_t i = a; i < e; ++i) acc += row[i];
+  uint32_t total;
+  uint32_t run = block_excl_scan_256(acc, &total);
+  for (uint32_t i = a; i < e; ++i) {
+    const uint32_t v = row[i];
+    row[i] = run;
+    run += v;
+  }
+  if (t == 0) *run_counter(rc, (int)blockIdx.x) = total;
+}
+
+__global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, int bucket_thr, uint32_t ntiles,
+                                                    const uint64_t* __restrict__ hbits,
+                                                    const uint32_t* __restrict__ tail_ends,
+                                                    const uint32_t* __restrict__ counts,
+                                                    MergeWork w) {
+  __shared__ uint64_t hb[kRunTile / 64];
+  __shared__ uint32_t lbase[kRunLists], lfill[kRunLists];
+  const uint32_t t = threadIdx.x;
+  const uint32_t T0 = blockIdx.x * kRunTile;
+  if (t < kRunTile / 64) hb[t] = hbits[(size_t)blockIdx.x * (kRunTile / 64) + t];
+  if (t < (uint32_t)kRunLists) {
+    lbase[t] = counts[(size_t)t * ntiles + blockIdx.x];
+    lfill[t] = 0u;
+  }
   __syncthreads();
-  for (int k = 0; k < kRunTile / 256; ++k) {
+  const uint32_t tail_end = tail_ends[blockIdx.x];
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
     const uint32_t q = (uint32_t)k * 256u + t;
     if ((hb[q >> 6] >> (q & 63u)) & 1ull) {
       uint32_t b;
-      const int l = run_at(q, b);
+      const int l = run_list(hb, T0, tail_end, q, bucket_thr, b);
       if (l < 0) continue;
       const uint32_t at = lbase[l] + atomicAdd(&lfill[l], 1u);
       const uint2 e = make_uint2(lo + T0 + q, b);
@@ -623,17 +761,6 @@ __device__ __forceinline__ void split8(const float* p, bool ok, bf16x8& hi, bf16
     hi[j] = h;
     lo[j] = (__bf16)(x[j] - (float)h);  // x - hi is exact in f32
   }
-}
-
-// Pre-screen of one pair from its Gram value: 1 = merge, 0 = no merge, 2 = too close to call
-// (or den outside the fast range): the exact sequential dot decides.
-__device__ __forceinline__ uint32_t prescreen(const Decider& dc, float g, float den) {
-  if (den >= 0x1p-60f && den <= 0x1p60f) {
-    const float q = g * __builtin_amdgcn_rcpf(den);
-    if (q >= dc.g_hi) return 1u;
-    if (q <= dc.g_lo) return 0u;
-  }
-  return 2u;
 }
 
 // One wave: the decisions of rows [R*64, R*64+64) against rows [C*64, C*64+64) (C <= R; pairs
@@ -947,6 +1074,279 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
   }
 }
 
+// The same walk for runs whose rows sit in LDS at a register width (D = 8..64), built around ONE
+// workgroup barrier per merge step (big_walk needs four):
+//  * positions are owned statically — lane t holds positions t, t + NT, ... — with their rows in
+//    registers (a row at a position >= i never changes; only the row moved into position i by the
+//    swap-remove is reloaded, by its one owner);
+//  * the owner of a position updates its P row after a merge and tests it at once, so the next
+//    merge (its position, first matching position j, and both row ids) is a wave ballot + one
+//    64-bit word per wave in LDS, read by every wave after the barrier;
+//  * every wave computes the merge itself (consensus into a wave-private copy of the new row, the
+//    member links by one lane) and applies the step's writes to the shared state (pos2row, counts,
+//    list heads, the new row) at the START of the next step: every wave writes the same values,
+//    each before its own reads, so no wave can see a half-written step and no second barrier is
+//    needed;
+//  * the decisions against the new row come from short chains (four interleaved partial sums of
+//    its norm and of each dot product, |error| <= 2 * 64 * 2^-24 |a||b| each — far inside
+//    kGramMargin), settled by the same certified pre-screen as the Gram tiles; only pairs within
+//    the margin of the threshold run the reference's sequential chains.  The new row's exact norm
+//    (distance.cc:33-34) is needed by nobody during the walk — rows at positions below i are never
+//    tested again — so it is computed once per rewritten row at the write-back.
+template <int RB, int NT, int D>
+__device__ __forceinline__ void big_walk_reg(uint32_t p, uint32_t b, uint64_t* P, uint32_t* slot,
+                                             float* nrm, uint32_t* cnt, uint32_t* hd, uint32_t* tl,
+                                             uint32_t* pos2row, float* sq, float* rowsL,
+                                             float* cwall, uint64_t* wbuf, const Rows& r,
+                                             const Decider& dc, uint32_t* slots, uint32_t* dlist,
+                                             Counters* ctr) {
+  constexpr int W = RB / 64, NW = NT / 64, KP = (RB + NT - 1) / NT, ST = D + 4;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  constexpr uint64_t kNone64 = ~0ull;
+  static_assert(RB <= 1024, "positions are packed in 10 bits");
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  float* cw = cwall + wv * 64;  // this wave's copy of the newest row
+  float xr[KP][D];              // the rows at my positions t + kp * NT
+  uint32_t yr[KP];              // their row ids
+  float sqy[KP];                // their sqrtf(norm)
+#pragma unroll
+  for (int kp = 0; kp < KP; ++kp) {
+    const uint32_t q = t + (uint32_t)kp * NT;
+    yr[kp] = q;
+    sqy[kp] = 0.0f;
+    if (q < b) {
+      load_row<D>(rowsL + q * ST, xr[kp]);
+      sqy[kp] = sq[q];
+    }
+  }
+  // the first position below q that row y (words w) matches, or kNone
+  auto first_below = [&](const uint64_t (&w)[W], uint32_t q) -> uint32_t {
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const uint32_t lo = (uint32_t)k * 64u;
+      if (lo < q) {
+        uint64_t m = w[k];
+        if (q - lo < 64u) m &= (1ull << (q - lo)) - 1ull;
+        if (m) return lo + (uint32_t)__builtin_ctzll(m);
+      }
+    }
+    return kNone;
+  };
+  // a hit: (position << 20 | its first match << 10 | its row) << 32 | the matching row
+  auto pack = [](uint32_t q, uint32_t j, uint32_t y, uint32_t c) -> uint64_t {
+    return ((uint64_t)((q << 20) | (j << 10) | y) << 32) | c;
+  };
+  // the wave's first hit (lowest position: kp-major, then lane order) -> wbuf[par][wv]
+  auto publish = [&](uint32_t par, const uint64_t (&hit)[KP]) {
+    uint64_t best = kNone64;
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      const uint64_t m = __ballot(hit[kp] != kNone64);
+      if (m && best == kNone64) best = shfl64(hit[kp], (uint32_t)__builtin_ctzll(m));
+    }
+    if (lane == 0) wbuf[par * NW + wv] = best;
+  };
+  uint32_t size = b, par = 0;
+  {
+    uint64_t hit[KP];
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      const uint32_t q = t + (uint32_t)kp * NT;
+      hit[kp] = kNone64;
+      if (q >= 1 && q < b) {
+        uint64_t w[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) w[k] = P[q * W + k];
+        const uint32_t j = first_below(w, q);
+        if (j != kNone) hit[kp] = pack(q, j, q, j);  // positions are the rows before any merge
+      }
+    }
+    publish(par, hit);
+  }
+  lds_barrier();
+  // the previous step's writes, applied by every wave at the start of the next step
+  bool have = false;
+  uint32_t ip = 0, mp = 0, cp = 0, rp = 0, cntp = 0, hdp = 0;
+  float cvp = 0.0f;
+  [[maybe_unused]] uint64_t steps = 0, wp[6] = {0, 0, 0, 0, 0, 0}, ck = WPROF_CLK(), ck1 = 0;
+  while (true) {
+    uint64_t best = kNone64;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) best = min(best, wbuf[par * NW + w]);
+    par ^= 1u;
+    if (have) {
+      if (lane == 0) {
+        pos2row[ip] = mp;
+        cnt[cp] = cntp;
+        cnt[rp] = 0u;
+        hd[cp] = hdp;
+      }
+      if (lane < (uint32_t)D) rowsL[cp * ST + lane] = cvp;
+      wave_lds_fence();
+    }
+    if (best == kNone64) break;
+    ++steps;
+    const uint32_t hi = (uint32_t)(best >> 32);
+    const uint32_t i = hi >> 20, j = (hi >> 10) & 1023u, rr = hi & 1023u, c = (uint32_t)best;
+    const uint32_t moved = pos2row[size - 1];
+    const uint32_t ca = cnt[rr], cb = cnt[c], hr = hd[rr], tr = tl[rr], hc = hd[c];
+#ifdef KLSH_MERGE_PROF
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ck1 = WPROF_CLK(); wp[0] += ck1 - ck; ck = ck1;
+#endif
+    // consensus (funcAB.cc:65), current row first, into this wave's copy of the new row c
+    const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
+    float cv = 0.0f;
+    if (lane < (uint32_t)D) {
+      cv = consensus(rowsL[rr * ST + lane], fa, rowsL[c * ST + lane], fb, fn);
+      cw[lane] = cv;
+    }
+    if (t == 0) r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
+    wave_lds_fence();
+    --size;  // swap-remove: the row at the old last position (size) moves to position i
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      if (t + (uint32_t)kp * NT == i && i < size) {
+        yr[kp] = moved;
+        load_row<D>(rowsL + moved * ST, xr[kp]);
+        sqy[kp] = sq[moved];
+      }
+    }
+    float cvec[D];
+    load_row<D>(cw, cvec);
+#ifdef KLSH_MERGE_PROF
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ck1 = WPROF_CLK(); wp[1] += ck1 - ck; ck = ck1;
+#endif
+    // short chains: four interleaved partial sums (a screen, not the reference's order)
+    float n4[4] = {0.0f, 0.0f, 0.0f, 0.0f}, d4[KP][4];
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) d4[kp][0] = d4[kp][1] = d4[kp][2] = d4[kp][3] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      n4[k & 3] = n4[k & 3] + cvec[k] * cvec[k];
+#pragma unroll
+      for (int kp = 0; kp < KP; ++kp) d4[kp][k & 3] = d4[kp][k & 3] + xr[kp][k] * cvec[k];
+    }
+    const float sc_a = __builtin_sqrtf((n4[0] + n4[1]) + (n4[2] + n4[3]));
+    uint32_t dn[KP];
+    bool amb = false;
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      const uint32_t q = t + (uint32_t)kp * NT;
+      dn[kp] = 0u;
+      if (q >= i && q < size) {
+        const float dot_a = (d4[kp][0] + d4[kp][1]) + (d4[kp][2] + d4[kp][3]);
+        dn[kp] = dc.fast ? prescreen(dc, dot_a, sqy[kp] * sc_a) : 2u;
+        amb = amb || dn[kp] == 2u;
+      }
+    }
+    if (__ballot(amb)) {  // rare: the reference's sequential chains settle the close calls
+      float nn = 0.0f;
+#pragma unroll
+      for (int k = 0; k < D; ++k) nn = nn + cvec[k] * cvec[k];
+      const float sc = __builtin_sqrtf(nn);
+#pragma unroll
+      for (int kp = 0; kp < KP; ++kp) {
+        if (dn[kp] == 2u) {
+          float dot = 0.0f;
+#pragma unroll
+          for (int k = 0; k < D; ++k) dot = dot + xr[kp][k] * cvec[k];
+          dn[kp] = decide(dc, dot, sqy[kp] * sc) ? 1u : 0u;
+        }
+      }
+    }
+#ifdef KLSH_MERGE_PROF
+    asm volatile("s_nop 0" ::"v"(dn[0]) : "memory");
+    ck1 = WPROF_CLK(); wp[2] += ck1 - ck; ck = ck1;
+#endif
+    uint64_t hit[KP];
+#pragma unroll
+    for (int kp = 0; kp < KP; ++kp) {
+      const uint32_t q = t + (uint32_t)kp * NT;
+      hit[kp] = kNone64;
+      if (q >= i && q < size) {
+        const uint32_t y = yr[kp];
+        uint64_t w[W];
+#pragma unroll
+        for (int k = 0; k < W; ++k) w[k] = P[y * W + k];
+        // position-space bits: the moved row's bit goes to position i, bit j is re-decided
+        const bool bm = (w[size >> 6] >> (size & 63u)) & 1ull;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          uint64_t v = w[k];
+          if ((uint32_t)k == (size >> 6)) v &= ~(1ull << (size & 63u));
+          if ((uint32_t)k == (i >> 6)) v = bm ? (v | (1ull << (i & 63u))) : (v & ~(1ull << (i & 63u)));
+          if ((uint32_t)k == (j >> 6))
+            v = dn[kp] ? (v | (1ull << (j & 63u))) : (v & ~(1ull << (j & 63u)));
+          if (v != w[k]) P[y * W + k] = v;
+          w[k] = v;
+        }
+        const uint32_t jj = first_below(w, q);
+        // the row at position jj as of this step (position i now holds the moved row)
+        if (jj != kNone) hit[kp] = pack(q, jj, y, jj == i ? moved : pos2row[jj]);
+      }
+    }
+    publish(par, hit);
+    have = true;
+    ip = i;
+    mp = moved;
+    cp = c;
+    rp = rr;
+    cntp = ca + cb;
+    hdp = hr;
+    cvp = cv;
+#ifdef KLSH_MERGE_PROF
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ck1 = WPROF_CLK(); wp[3] += ck1 - ck; ck = ck1;
+#endif
+    lds_barrier();
+#ifdef KLSH_MERGE_PROF
+    ck1 = WPROF_CLK(); wp[5] += ck1 - ck; ck = ck1;
+#endif
+  }
+#ifdef KLSH_MERGE_PROF
+  if (t == 0) {
+    const int cls = RB <= 128 ? 0 : RB <= 192 ? 1 : 2;
+    atomicAdd(&g_wprof[cls][4], (unsigned long long)steps);
+    for (int k = 0; k < 4; ++k) atomicAdd(&g_wprof[cls][k], (unsigned long long)wp[k]);
+    atomicAdd(&g_wprof[cls][5], (unsigned long long)wp[5]);
+  }
+#endif
+  __syncthreads();
+  // write back: survivors in position order, kInvalid after; rewritten rows; metadata
+  for (uint32_t q = t; q < b; q += NT) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
+  {  // a survivor was rewritten iff its count rose (the global count is still old)
+    constexpr uint32_t c4 = (uint32_t)D / 4;
+    for (uint32_t idx = t; idx < size * c4; idx += NT) {
+      const uint32_t q = idx / c4, k = (idx % c4) * 4;
+      const uint32_t y = pos2row[q];
+      if (r.cnt[slot[y]] != cnt[y])
+        *reinterpret_cast<float4*>(r.x + (size_t)slot[y] * r.dp + k) =
+            *reinterpret_cast<const float4*>(rowsL + y * ST + k);
+    }
+    __syncthreads();
+  }
+  for (uint32_t q0 = 0; q0 < size; q0 += NT) {  // uniform trip count (ballot inside)
+    const uint32_t q = q0 + t;
+    bool rewritten = false;
+    if (q < size) {
+      const uint32_t y = pos2row[q];
+      rewritten = r.cnt[slot[y]] != cnt[y];  // every merge into a row raises its count
+      float nv = nrm[y];
+      if (rewritten) {  // the exact sequential norm of the new row (distance.cc:33-34)
+        nv = 0.0f;
+#pragma unroll
+        for (int k = 0; k < D; ++k) nv = nv + rowsL[y * ST + k] * rowsL[y * ST + k];
+      }
+      r.nrm[slot[y]] = nv;
+      r.cnt[slot[y]] = cnt[y];
+      r.head[slot[y]] = hd[y];
+    }
+    if (dlist) append_slot(rewritten, q < size ? slot[pos2row[q]] : 0u, dlist, &ctr->n_delta);
+  }
+}
+
 template <int D, int RB, bool ROWS_LDS>
 struct BigLayout {
   static constexpr int ST = D + 4;
@@ -977,6 +1377,8 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
   uint32_t* pos2row = slot + 5 * RB;
   float* sq = reinterpret_cast<float*>(slot + 6 * RB);  // sqrtf(nrm), distance.cc:37
   __shared__ uint32_t wbuf[2 * NW];
+  __shared__ __attribute__((aligned(16))) float cwall[NW * 64];  // big_walk_reg's new-row copies
+  __shared__ uint64_t wbuf64[2 * NW];                              // big_walk_reg's published hits
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   auto row_ptr = [&](uint32_t a) -> const float* {
     return ROWS_LDS ? rows + a * ST : r.x + (size_t)slot[a] * r.dp;
@@ -1081,8 +1483,14 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
     }
     __syncthreads();
     [[maybe_unused]] const uint64_t pt1 = MPROF_T();
-    big_walk<RB, NT, ROWS_LDS, D>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq,
-                               ROWS_LDS ? rows : nullptr, ST, rows, wbuf, r, dc, slots, dlist, ctr);
+    if constexpr (ROWS_LDS && D > 0 && D <= 64) {
+      big_walk_reg<RB, NT, D>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq, rows, cwall, wbuf64, r,
+                              dc, slots, dlist, ctr);
+    } else {
+      big_walk<RB, NT, ROWS_LDS, D>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq,
+                                 ROWS_LDS ? rows : nullptr, ST, rows, wbuf, r, dc, slots, dlist,
+                                 ctr);
+    }
     __syncthreads();
 #ifdef KLSH_MERGE_PROF
     if (t == 0) {
@@ -1773,7 +2181,11 @@ struct Fork {
   hipStream_t s;
   bool on;
   Fork(const MergeWork& w_, hipStream_t s_) : w(w_), s(s_) {
+#ifdef KLSH_SERIAL_MERGE  // diagnostics build only: every class in order on the main stream
+    on = false;
+#else
     on = w.aux[0] != nullptr;
+#endif
     if (!on) return;
     (void)hipEventRecord(w.fork, s);
     for (int i = 0; i < kMergeStreams; ++i) (void)hipStreamWaitEvent(w.aux[i], w.fork, 0);
@@ -1870,7 +2282,14 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   if (hi <= lo) return;
   const uint32_t n = hi - lo;
   const Decider dc = make_decider(thr);
-  k_runs<<<(n + kRunTile - 1) / kRunTile, 256, 0, s>>>(key, lo, n, bucket_thr, w);
+  const uint32_t ntiles = (n + kRunTile - 1) / kRunTile;
+  uint32_t* counts = w.run_ws;
+  uint32_t* tail_ends = counts + (size_t)kRunRows * ntiles;
+  // 8-byte aligned: counts + tail ends take 14 * ntiles words, rounded up to even
+  uint64_t* hbits = reinterpret_cast<uint64_t*>(counts + ((14u * ntiles + 1u) & ~1u));
+  k_runs_count<<<ntiles, 256, 0, s>>>(key, lo, n, bucket_thr, ntiles, hbits, tail_ends, counts);
+  k_runs_scan<<<kRunRows, 256, 0, s>>>(counts, ntiles, w.rc);
+  k_runs_write<<<ntiles, 256, 0, s>>>(lo, bucket_thr, ntiles, hbits, tail_ends, counts, w);
   switch (r.d) {
     case 8: launch_groups<8>(r, slots, dc, w, ctr, n, s); break;
     case 16: launch_groups<16>(r, slots, dc, w, ctr, n, s); break;
@@ -1897,8 +2316,8 @@ void merge_prof_dump(FILE* f) {
   if (hipMemcpyFromSymbol(wpf, HIP_SYMBOL(g_wprof), sizeof(wpf)) == hipSuccess)
     for (int c = 0; c < kBigClasses; ++c)
       if (wpf[c][4])
-        fprintf(f, "[wprof] %-7s steps %9llu  clocks/step: find %7.0f  select+consensus %7.0f"
-                   "  dots %7.0f  bits %7.0f   find rounds/step %.2f\n",
+        fprintf(f, "[wprof] %-7s steps %9llu  clocks/step: find|select %7.0f  select+consensus|consensus %7.0f"
+                   "  dots %7.0f  bits %7.0f   find rounds/step|barrier clocks %.2f\n",
                 names[c], wpf[c][4], (double)wpf[c][0] / wpf[c][4], (double)wpf[c][1] / wpf[c][4],
                 (double)wpf[c][2] / wpf[c][4], (double)wpf[c][3] / wpf[c][4],
                 (double)wpf[c][5] / wpf[c][4]);
