@@ -223,14 +223,14 @@ def check_parity(config, trace, counter, result):
     return out
 
 
-def pmc_traffic(config):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+def pmc_traffic(config, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         data = json.load(f)
-    return data.get(config)
+    return (data.get(config) or {}).get(kernel)
 
 
 def main():
@@ -293,34 +293,54 @@ def main():
     value = (1 if sharded else world) * n0 * iters * args.steps / elapsed
     agg = {k: sum(s[k] for s in stats) for k in stats[0]}
     phases = {p: agg[p + "_ms"] / args.steps
-              for p in ("project", "sort", "merge", "compact", "host", "comm")}
-    # dominant kernel: the projection (k_project<64>) unless another phase dominates
+              for p in ("project", "sort", "merge", "compact", "host", "comm", "small")}
+    # Kernel rooflines.  The projection: algorithmic bytes per launch = rows x
+    # (4d row + 4 slot + 4 key).  The small-run merge (runs of 2..64 rows; its own launch in the
+    # iterations of >= 2^20 positions, ~83 ms of a C2 step, timed by HIP events on its stream):
+    # rows x (4d row + 4 slot) + merges x (4d new row + 20 metadata: norm, count, head, member
+    # link, the removed row's count) — merges counted over the whole iteration (~97 % of them are
+    # small-run merges on C2).  The bench line's "roofline" is the one with the larger time per step.
     launches = agg["project_launches"]
     proj_bytes = agg["sum_rows"] * (4 * d + 8)      # row read + slot read + key write
     avg_ms = agg["project_ms"] / max(1, launches)
     achieved = (proj_bytes / max(1, launches)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = pmc_traffic(args.config)
     # the same launches against the packed-f32 VALU ceiling: one v_pk_mul + one v_pk_add per two
     # row-hyperplane MACs (bit-exactness forbids fusing), 256 CU x 4 SIMD x 16 lanes x 2 x 2 flop
     # x 2.4 GHz = 78.6 Tflop/s (half the FMA-counted 157.3 TF vector peak)
     valu_flops = 2.0 * agg["sum_proj_bits"] * d / max(1, launches)
     valu_achieved = valu_flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    roofline = {
-        "kernel": f"k_project_pk<{d}>" if d in (8, 16, 32, 64) else "k_project_wide_pk",
-        "bound": "hbm",
-        "achieved": round(achieved, 2),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 5),
-        "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
-        "traffic_source": (traffic or {}).get("source"),
-        "bytes_per_launch": proj_bytes / max(1, launches),
-        "avg_launch_ms": avg_ms,
-        "launches_per_step": launches / args.steps,
+    pname = f"k_project_pk<{d}>" if d in (8, 16, 32, 64) else "k_project_mfma_wide"
+    ptraffic = pmc_traffic(args.config, "k_project")
+    project = {
+        "kernel": pname, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "traffic": ptraffic.get("hbm_bytes_per_launch") if ptraffic else None,
+        "traffic_source": (ptraffic or {}).get("source"),
+        "bytes_per_launch": proj_bytes / max(1, launches), "avg_launch_ms": avg_ms,
+        "launches_per_step": launches / args.steps, "ms_per_step": agg["project_ms"] / args.steps,
         "valu": {"achieved": round(valu_achieved, 2), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                  "frac": round(valu_achieved / VALU_PEAK_TFLOPS, 4),
                  "note": "separate f32 mul+add (no FMA: bit-exact with the reference), packed"},
     }
+    kernels = [project]
+    if agg.get("small_launches"):
+        sl = agg["small_launches"]
+        s_bytes = agg["small_rows"] * (4 * d + 4) + agg["small_iter_merges"] * (4 * d + 20)
+        s_ms = agg["small_ms"] / sl
+        s_ach = (s_bytes / sl) / (s_ms * 1e-3) / 1e9 if s_ms > 0 else 0.0
+        straffic = pmc_traffic(args.config, "k_merge_small")
+        kernels.append({
+            "kernel": f"k_merge_small<{d}>", "bound": "hbm", "achieved": round(s_ach, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(s_ach / HBM_PEAK_GBS, 5),
+            "traffic": straffic.get("hbm_bytes_per_launch") if straffic else None,
+            "traffic_source": (straffic or {}).get("source"),
+            "bytes_per_launch": s_bytes / sl, "avg_launch_ms": s_ms,
+            "launches_per_step": sl / args.steps, "ms_per_step": agg["small_ms"] / args.steps,
+            "rows_per_launch": agg["small_rows"] / sl,
+            "note": "the iterations of >= 2^20 positions (below that the small runs merge inside "
+                    "k_merge_tail with the big runs)"})
+    roofline = dict(max(kernels, key=lambda k: k["ms_per_step"]))
+    roofline["kernels"] = kernels
     # the whole loop against HBM, SURVEY.md §8(d): B_t = N_t (8d + 16) + M_t (4d + 8) bytes per
     # iteration (rows read by the projection and by the merge, keys and order written and read;
     # per merge the new row and a member link), summed over the timed steps

@@ -57,6 +57,13 @@ typedef struct klsh_stats {
   double host_ms;          /* host-side hyperplane generation */
   double comm_ms;          /* sharded loop: host time in inter-rank exchanges (incl. waits) */
   uint64_t world;          /* ranks the call ran on (1 = single GPU) */
+  /* the small-run merge (runs of 2..64 rows) of the iterations where it is a launch of its own
+   * (>= 2^20 positions): HIP-event time on its stream, launches, rows in those runs, merges of
+   * the whole iteration (small-run merges are ~97% of them on C2) */
+  double small_ms;
+  uint64_t small_launches;
+  uint64_t small_rows;
+  uint64_t small_iter_merges;
 } klsh_stats;
 
 /* ---- lifetime ------------------------------------------------------------------------------- */
@@ -110,7 +117,9 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  * remaining iterations on its own replica, without exchanges; default 2097152 = 2^21, 0 = always
  * sharded), "phase_timing" (0/1: per-phase HIP events, adds latency) — results never depend on
  * either; "stop_after" (k > 0: klsh_cluster runs only the first k iterations of its threshold
- * schedule, e.g. to pin a prefix of a long loop; 0 = all, the default). */
+ * schedule, e.g. to pin a prefix of a long loop; 0 = all, the default), "hyperplane_window"
+ * (hyperplane rows drawn up front per call; the rest are drawn when the loop reaches them; 0 =
+ * the default: all of them while they fit in 256 MB, else 64 iterations' worth). */
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
 
 /* ---- results ---------------------------------------------------------------------------------- */

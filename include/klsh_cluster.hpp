@@ -69,7 +69,6 @@ void Cluster(std::vector<Abundance*>* rows, float min_similarity, int cluster_it
     std::copy(a->_values.begin(), a->_values.begin() + dim, x.begin() + i * dim);
     off[i + 1] = off[i] + a->_ids.size();
     ids.insert(ids.end(), a->_ids.begin(), a->_ids.end());
-    delete a;
   }
   check(klsh_load_rows(P.ctx, x.data(), n, dim, off.data(), ids.data()), "klsh_load_rows");
   std::vector<uint64_t> trace(cluster_iteration > 0 ? cluster_iteration : 1);
@@ -88,6 +87,9 @@ void Cluster(std::vector<Abundance*>* rows, float min_similarity, int cluster_it
   off.assign(nout + 1, 0);
   ids.resize(m);
   check(klsh_result(P.ctx, x.data(), off.data(), ids.data()), "klsh_result");
+  // only now are the input rows released: a failure above leaves *rows as it was (still owned by
+  // the caller), never holding freed pointers
+  for (Abundance* a : *rows) delete a;
   rows->clear();
   rows->reserve(nout);
   for (uint64_t i = 0; i < nout; ++i) {

@@ -54,6 +54,10 @@ class KlshStats(ctypes.Structure):
         ("host_ms", ctypes.c_double),
         ("comm_ms", ctypes.c_double),
         ("world", ctypes.c_uint64),
+        ("small_ms", ctypes.c_double),
+        ("small_launches", ctypes.c_uint64),
+        ("small_rows", ctypes.c_uint64),
+        ("small_iter_merges", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -25,17 +25,28 @@ struct RcclComm final : Comm {
   ~RcclComm() override {
     if (nc) (void)ncclCommDestroy(nc);
   }
+  void abort() override {
+    aborted = true;
+    if (nc) (void)ncclCommAbort(nc);
+    nc = nullptr;
+  }
   int check(ncclResult_t r, const char* what) {
+    if (aborted) {
+      err = std::string(what) + ": communicator aborted";
+      return -1;
+    }
     if (r == ncclSuccess) return 0;
     err = std::string(what) + ": " + ncclGetErrorString(r);
     return -1;
   }
   int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     if (bytes == 0) return 0;
+    if (aborted) return check(ncclSuccess, "ncclAllGather");
     return check(ncclAllGather(send, recv, bytes, ncclChar, nc, s), "ncclAllGather");
   }
   int allgatherv(const void* send, void* recv, const size_t* counts, const size_t* offs,
                  hipStream_t s) override {
+    if (aborted) return check(ncclSuccess, "allgatherv");
     int rc = check(ncclGroupStart(), "ncclGroupStart");
     for (int r = 0; r < world && !rc; ++r) {
       if (counts[r] == 0) continue;
@@ -48,6 +59,7 @@ struct RcclComm final : Comm {
   }
   int alltoallv(const void* send, const size_t* scnt, const size_t* soff, void* recv,
                 const size_t* rcnt, const size_t* roff, hipStream_t s) override {
+    if (aborted) return check(ncclSuccess, "alltoallv");
     // the rank's own piece is a local copy
     if (scnt[rank]) {
       if (hipMemcpyAsync(static_cast<char*>(recv) + roff[rank],
@@ -72,6 +84,7 @@ struct RcclComm final : Comm {
   }
   int allreduce_min_u32(uint32_t* buf, size_t n, hipStream_t s) override {
     if (n == 0) return 0;
+    if (aborted) return check(ncclSuccess, "ncclAllReduce");
     return check(ncclAllReduce(buf, buf, n, ncclUint32, ncclMin, nc, s), "ncclAllReduce");
   }
 };
@@ -118,20 +131,29 @@ struct Hub {
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
+  bool aborted = false;  // a rank failed: every barrier returns at once
   // what each rank posted for the current collective
   std::vector<const void*> ptr;
   std::vector<const size_t*> vec;
   explicit Hub(int w) : world(w), ptr(w, nullptr), vec(w, nullptr) {}
-  void barrier() {
+  // false if the group was aborted (by any rank)
+  bool barrier() {
     std::unique_lock<std::mutex> lk(m);
+    if (aborted) return false;
     const uint64_t g = gen;
     if (++arrived == world) {
       arrived = 0;
       ++gen;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return gen != g; });
+      cv.wait(lk, [&] { return gen != g || aborted; });
     }
+    return !aborted;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(m);
+    aborted = true;
+    cv.notify_all();
   }
 };
 
@@ -142,6 +164,10 @@ struct LocalComm final : Comm {
   const char* kind() const override { return "local"; }
   ~LocalComm() override {
     if (tmp) (void)hipFree(tmp);
+  }
+  void abort() override {
+    aborted = true;
+    hub->abort();
   }
   int sync(hipStream_t s) {
     if (hipStreamSynchronize(s) != hipSuccess) {
@@ -165,10 +191,16 @@ struct LocalComm final : Comm {
     if (int e = sync(s)) return e;  // my send data is complete
     hub->ptr[rank] = p;
     hub->vec[rank] = v;
-    hub->barrier();
+    if (!hub->barrier()) {
+      err = "local comm: group aborted";
+      return -1;
+    }
     int rc = body();
     if (!rc) rc = sync(s);
-    hub->barrier();
+    if (!hub->barrier() && !rc) {
+      err = "local comm: group aborted";
+      rc = -1;
+    }
     return rc;
   }
   int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {

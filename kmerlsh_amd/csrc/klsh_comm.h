@@ -40,6 +40,11 @@ struct Comm {
                         const size_t* rcnt, const size_t* roff, hipStream_t s) = 0;
   // buf[i] = min over ranks of buf[i] (n uint32 elements), in place.
   virtual int allreduce_min_u32(uint32_t* buf, size_t n, hipStream_t s) = 0;
+  // After a local failure mid-call: make the group's pending and later collectives fail instead
+  // of waiting forever for this rank (RCCL: ncclCommAbort; in-process group: wake every waiter).
+  // The communicator is unusable afterwards.
+  virtual void abort() = 0;
+  bool aborted = false;
   std::string err;
 };
 

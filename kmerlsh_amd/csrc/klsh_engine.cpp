@@ -96,6 +96,7 @@ struct klsh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
+  hipEvent_t sev[2] = {};  // around the small-run merge launch (bench roofline)
 
   // sizes
   int d = 0, dp = 0;
@@ -184,6 +185,8 @@ struct klsh_ctx {
   // schedule (0 = all).  Prefix parity tests of the long configs use it; results of the
   // iterations that do run are unchanged.
   int stop_after = 0;
+  // "hyperplane_window" (klsh_set_option): rows drawn up front per call (0 = the default bound)
+  uint64_t hyperplane_window = 0;
 
   int world() const { return comm ? comm->world : 1; }
   int rank() const { return comm ? comm->rank : 0; }
@@ -268,6 +271,8 @@ struct klsh_ctx {
     pub_host = nullptr;
     pub_dev = nullptr;
     for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    for (auto& e : sev)
       if (e) (void)hipEventDestroy(e), e = nullptr;
     for (int i = 0; i < klsh::kMergeStreams; ++i) {
       if (mw.join[i]) (void)hipEventDestroy(mw.join[i]);
@@ -370,6 +375,17 @@ struct klsh_ctx {
     return 0;
   }
   const float* hyperplane_ptr(uint64_t k) const { return W + (k - w_k0) * (uint64_t)dp; }
+  // The hyperplanes of the first iterations of a call, drawn up front: every iteration's h_t
+  // (<= hmax) for all of them when that fits in 64 Mi floats (256 MB: C2 draws 11.5 K rows of 64),
+  // else the first 64 iterations' worth — ensure_hyperplanes extends the window when the loop
+  // gets there (-I 10000 at d = 4096 would otherwise need ~3.8 GB up front, host and device).
+  int predraw_hyperplanes(uint32_t base, uint64_t k0, uint64_t hmax, int iterations,
+                          double* host_ms) {
+    const uint64_t want = hmax * (uint64_t)iterations;
+    const uint64_t cap = hyperplane_window ? hyperplane_window
+                                           : std::max<uint64_t>(hmax * 64, (64ull << 20) / (uint64_t)dp);
+    return ensure_hyperplanes(base, k0, std::min(want, cap), host_ms);
+  }
 
   // zero the iteration counters (and the run-list counters) on the stream
   int reset_counters() {
@@ -469,6 +485,7 @@ klsh_ctx* klsh_create(int device, int* err) {
   bool ok = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking,
                                         big_prio ? prio_hi : prio_lo) == hipSuccess;
   for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  for (auto& e : c->sev) ok = ok && hipEventCreate(&e) == hipSuccess;
   for (int i = 0; i < klsh::kMergeStreams; ++i) {
     ok = ok && hipStreamCreateWithPriority(&c->mw.aux[i], hipStreamNonBlocking,
                                            (i == 0 && big_prio) ? prio_hi : prio_lo) == hipSuccess;
@@ -681,7 +698,13 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
                       bool sync = true, const std::function<int(uint32_t*)>* after = nullptr) {
   hipStream_t s = ctx->stream;
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
+  // the small-run merge is a launch of its own at >= 2^20 positions (register widths): time it
+  const bool time_small = st && sync && !ctx->comm && n >= (1u << 20) &&
+                          klsh::project_device_n_ok(ctx->d);
+  ctx->mw.small_ev[0] = time_small ? ctx->sev[0] : nullptr;
+  ctx->mw.small_ev[1] = time_small ? ctx->sev[1] : nullptr;
   klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->mw, ctx->ctr, s);
+  ctx->mw.small_ev[0] = ctx->mw.small_ev[1] = nullptr;
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[3], s));
   const bool zc = sync && ctx->zero_copy;
@@ -698,6 +721,13 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   } else {
     ctx->ctr_clean = false;
     if (int e = ctx->sync_counters()) return e;
+  }
+  if (time_small) {  // the compaction (published) runs after the merge streams' join
+    KLSH_HIP(hipEventSynchronize(ctx->sev[1]));
+    st->small_ms += elapsed(ctx->sev[0], ctx->sev[1]);
+    st->small_launches += 1;
+    st->small_rows += ctx->h_ctr->n_small_rows;
+    st->small_iter_merges += n - ctx->h_ctr->total;
   }
   if (timed && zc) KLSH_HIP(hipEventSynchronize(ctx->ev[4]));
   if (timed && st) {
@@ -907,9 +937,9 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
 // then local order: a small allgather of (runs, hyperplanes) gives each rank its RNG offset.
 // Member links are written only by the rank that merged them; the end of the call combines them
 // with an element-wise min (an unwritten link is kNil = 0xFFFFFFFF) and gathers the global order.
-static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations, int run_iters,
-                           int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
-                           uint64_t* nt_trace, klsh_stats* st) {
+static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterations,
+                                int run_iters, int bucket_size_threshold, uint32_t seed_base,
+                                uint64_t* rng_counter, uint64_t* nt_trace, klsh_stats* st) {
   klsh::Comm* cm = ctx->comm;
   const int W = cm->world, g = cm->rank;
   hipStream_t s = ctx->stream;
@@ -945,9 +975,8 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations, 
 
   ctx->w_count = 0;
   if (N > 0 && iterations > 0) {
-    const uint64_t hmax = (uint64_t)floor_log2(N);
-    if (int e = ctx->ensure_hyperplanes(seed_base, *rng_counter, hmax * (uint64_t)iterations,
-                                        &st->host_ms))
+    if (int e = ctx->predraw_hyperplanes(seed_base, *rng_counter, (uint64_t)floor_log2(N),
+                                         iterations, &st->host_ms))
       return e;
   }
   const int R = klsh::delta_words(ctx->dp);
@@ -1153,10 +1182,30 @@ static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations, 
   return 0;
 }
 
+// A rank that fails mid-call aborts the group, so the other ranks' pending and next collectives
+// fail too instead of waiting for it forever; the context's group is unusable afterwards.
+static int cluster_sharded(klsh_ctx* ctx, float min_similarity, int iterations, int run_iters,
+                           int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
+                           uint64_t* nt_trace, klsh_stats* st) {
+  if (ctx->comm->aborted) return fail(KLSH_E_STATE, "communicator aborted by an earlier failure");
+  const int rc = cluster_sharded_body(ctx, min_similarity, iterations, run_iters,
+                                      bucket_size_threshold, seed_base, rng_counter, nt_trace, st);
+  if (rc) {
+    const std::string msg = g_err;
+    ctx->comm->abort();
+    ctx->mw.dlist = nullptr;
+    g_err = msg;
+  }
+  return rc;
+}
+
 int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket_size_threshold,
                  uint32_t seed_base, uint64_t* rng_counter, uint64_t* nt_trace, klsh_stats* stats) {
   if (!ctx || !rng_counter) return fail(KLSH_E_ARG, "null argument");
-  if (!ctx->loaded) return fail(KLSH_E_STATE, "klsh_cluster before a load");
+  if (!ctx->loaded) {
+    if (ctx->comm) ctx->comm->abort();  // the other ranks must not wait for this one
+    return fail(KLSH_E_STATE, "klsh_cluster before a load");
+  }
   KLSH_HIP(hipSetDevice(ctx->device));
   klsh_stats local{};
   klsh_stats* st = stats ? stats : &local;
@@ -1180,11 +1229,12 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
   // lshash.cc:36-42), so repeated timed calls never reuse a previous call's tables.
   ctx->w_count = 0;
-  // Pre-draw the hyperplanes this call can need without nested buckets (h_t is non-increasing).
+  // Pre-draw the hyperplanes this call can need without nested buckets (h_t is non-increasing),
+  // up to a bounded window; later ones are drawn when reached.
   if (ctx->n_live > 0 && iterations > 0) {
-    const uint64_t hmax = (uint64_t)floor_log2(ctx->n_live);
-    if (int e = ctx->ensure_hyperplanes(seed_base, *rng_counter, hmax * (uint64_t)iterations,
-                                        &st->host_ms))
+    if (int e = ctx->predraw_hyperplanes(seed_base, *rng_counter,
+                                         (uint64_t)floor_log2(ctx->n_live), iterations,
+                                         &st->host_ms))
       return e;
   }
 
@@ -1244,6 +1294,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   }
   if (n == "phase_timing") {
     ctx->phase_timing = value != 0;
+    return 0;
+  }
+  if (n == "hyperplane_window") {
+    if (value < 0) return fail(KLSH_E_ARG, "hyperplane_window must be >= 0");
+    ctx->hyperplane_window = (uint64_t)value;
     return 0;
   }
   if (n == "stop_after") {

@@ -46,12 +46,12 @@ struct alignas(128) CountLine {
   uint32_t pad_[31];
 };
 struct RunCounters {
-  CountLine n_seg, n_cls[kGroupClasses], n_big[kBigClasses], n_huge, n_over;
+  CountLine n_seg, n_cls[kGroupClasses], n_big[kBigClasses], n_huge, n_over, n_small_rows;
 };
 
 // Run-finding workspace (u32 words) for `slots` positions: 13 counts + a tail end + a 4096-bit
 // head bitmap per 4096-position tile.
-inline uint64_t run_ws_words(uint64_t slots) { return (slots / 4096 + 2) * (13 + 1 + 128) + 64; }
+inline uint64_t run_ws_words(uint64_t slots) { return (slots / 4096 + 2) * (14 + 1 + 128) + 64; }
 
 // Device-side per-iteration counters (zeroed by the host before each iteration).
 struct Counters {
@@ -63,7 +63,7 @@ struct Counters {
   uint32_t total;                  // result of the last scan/compaction (live rows)
   uint32_t n_delta;                // sharded loop: survivors rewritten by a merge this iteration
   uint32_t err;                    // a device-side protocol failure (look-back wait limit); 0 = ok
-  uint32_t pad;
+  uint32_t n_small_rows;           // rows in the runs of 2..64 rows (the small-run merge's rows)
 };
 
 // Merge workspace (device), sized for `cap` positions.
@@ -88,6 +88,7 @@ struct MergeWork {
   // the engine when the previous iteration had many of them (C4: thousands; C2: < 10)
   uint32_t big896_aux;
   hipStream_t aux[3];
+  hipEvent_t small_ev[2];  // timing events around the small-run launch (nullptr: not recorded)
   hipEvent_t fork;
   hipEvent_t join[3];
 };

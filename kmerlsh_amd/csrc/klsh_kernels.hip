@@ -711,6 +711,8 @@ __device__ __forceinline__ void collect_run_counts(Counters* ctr, RunCounters* r
   rc->n_huge.v = 0u;
   ctr->n_over = rc->n_over.v;
   rc->n_over.v = 0u;
+  ctr->n_small_rows = rc->n_small_rows.v;
+  rc->n_small_rows.v = 0u;
 }
 
 // Publish the iteration's counters to the host (see Publish), `total` filled in.

@@ -576,13 +576,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // positional.
 constexpr uint32_t kRunTile = 4096;
 constexpr int kRunLists = kGroupClasses + kBigClasses + 2;  // small classes, big classes, huge, over
-constexpr int kRunRows = kRunLists + 1;                      // + the head count (n_seg)
+constexpr int kRunRows = kRunLists + 2;  // + the head count (n_seg) + rows in small runs
 
 __device__ __forceinline__ uint32_t* run_counter(RunCounters* rc, int l) {
   return l < kGroupClasses ? &rc->n_cls[l].v
          : l < kGroupClasses + kBigClasses ? &rc->n_big[l - kGroupClasses].v
          : l == kRunLists - 2 ? &rc->n_huge.v
-         : l == kRunLists - 1 ? &rc->n_over.v : &rc->n_seg.v;
+         : l == kRunLists - 1 ? &rc->n_over.v
+         : l == kRunLists ? &rc->n_seg.v : &rc->n_small_rows.v;
 }
 
 // The run starting at tile-local position q (a head of bitmap hb): its length and list (-1: one row).
@@ -650,7 +651,7 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
   __syncthreads();
   const uint32_t tail_end = s_tail_end;
   const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-  uint32_t heads = 0;
+  uint32_t heads = 0, small_rows = 0;
 #pragma unroll 4
   for (int k = 0; k < 16; ++k) {
     const uint32_t q = (uint32_t)k * 256u + t;
@@ -659,6 +660,7 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
       uint32_t b;
       l = run_list(hb, T0, tail_end, q, bucket_thr, b);
       ++heads;
+      if (l >= 0 && l < kGroupClasses) small_rows += b;
     }
     // lanes with the same list: one LDS add by the lowest of them
     const uint32_t id = (uint32_t)(l + 1);  // 0 = no entry
@@ -671,8 +673,12 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
     if (l >= 0 && (match & lt) == 0ull) atomicAdd(&lcnt[l], (uint32_t)__popcll(match));
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) heads += __shfl_xor(heads, o, 64);
+  for (int o = 32; o > 0; o >>= 1) {
+    heads += __shfl_xor(heads, o, 64);
+    small_rows += __shfl_xor(small_rows, o, 64);
+  }
   if (lane == 0 && heads) atomicAdd(&lcnt[kRunLists], heads);
+  if (lane == 0 && small_rows) atomicAdd(&lcnt[kRunLists + 1], small_rows);
   __syncthreads();
   if (t < (uint32_t)kRunRows) counts[(size_t)t * ntiles + blockIdx.x] = lcnt[t];
 }
@@ -2238,7 +2244,9 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   launch_big<D, 192, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(1));
   launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   // every small-run class in one persistent launch (the kernel strides over its batches)
+  if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
   k_merge_small<D><<<4608, 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
+  if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[1], f.lane(2));
 }
 
 template <int RB, int NT, int KC>
@@ -2285,8 +2293,8 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   const uint32_t ntiles = (n + kRunTile - 1) / kRunTile;
   uint32_t* counts = w.run_ws;
   uint32_t* tail_ends = counts + (size_t)kRunRows * ntiles;
-  // 8-byte aligned: counts + tail ends take 14 * ntiles words, rounded up to even
-  uint64_t* hbits = reinterpret_cast<uint64_t*>(counts + ((14u * ntiles + 1u) & ~1u));
+  // 8-byte aligned: counts + tail ends take (kRunRows + 1) * ntiles words, rounded up to even
+  uint64_t* hbits = reinterpret_cast<uint64_t*>(counts + (((kRunRows + 1u) * ntiles + 1u) & ~1u));
   k_runs_count<<<ntiles, 256, 0, s>>>(key, lo, n, bucket_thr, ntiles, hbits, tail_ends, counts);
   k_runs_scan<<<kRunRows, 256, 0, s>>>(counts, ntiles, w.rc);
   k_runs_write<<<ntiles, 256, 0, s>>>(lo, bucket_thr, ntiles, hbits, tail_ends, counts, w);

@@ -7,10 +7,15 @@
 
 #include "klsh_cluster.hpp"
 
+#ifdef KLSH_REF_ABUNDANCE  // the reference's own data model, included in place (-D path)
+#include KLSH_REF_ABUNDANCE
+using Abundance = Core::Abundance;
+#else
 struct Abundance {  // same public members as the reference's Core::Abundance
   std::vector<float> _values;
   std::vector<uint64_t> _ids;
 };
+#endif
 
 int main(int argc, char** argv) {
   if (argc < 9) return 1;

@@ -11,14 +11,24 @@ from conftest import ROOT, golden
 SRC = os.path.join(ROOT, "tests", "cpp", "adapter_main.cpp")
 
 
-def build(out):
-    subprocess.run(["g++", "-std=c++11", "-O2", "-I", os.path.join(ROOT, "include"), SRC, "-o", out,
-                    "-L", os.path.join(ROOT, "kmerlsh_amd", "lib"), "-lklsh",
+REF_ABUNDANCE = "/root/reference/common/abundance.h"
+
+
+def build(out, defines=()):
+    subprocess.run(["g++", "-std=c++11", "-O2", *defines, "-I", os.path.join(ROOT, "include"), SRC,
+                    "-o", out, "-L", os.path.join(ROOT, "kmerlsh_amd", "lib"), "-lklsh",
                     "-Wl,-rpath," + os.path.join(ROOT, "kmerlsh_amd", "lib")], check=True)
 
 
 def test_adapter_compiles(tmp_path):
     build(str(tmp_path / "adapter"))
+
+
+@pytest.mark.skipif(not os.path.exists(REF_ABUNDANCE), reason="reference tree not present")
+def test_adapter_compiles_against_reference_abundance(tmp_path):
+    """The adapter instantiated with the reference's own Core::Abundance (common/abundance.h,
+    read in place), as app/kmerLSH.cc would after INTEGRATION.md's change: compile and link."""
+    build(str(tmp_path / "adapter_ref"), [f'-DKLSH_REF_ABUNDANCE="{REF_ABUNDANCE}"'])
 
 
 @pytest.mark.gpu

@@ -275,6 +275,24 @@ def test_cluster_random_vs_oracle(engine, oracle, n, d, groups, iters, bthr):
     assert_same_result(engine.result(), o_rows, o_off, o_ids)
 
 
+@pytest.mark.parametrize("window", [7, 40, 100])
+def test_cluster_small_hyperplane_window_vs_oracle(engine, oracle, window):
+    """Hyperplanes drawn in a bounded window (refilled when the loop reaches its end, also
+    under the queued-ahead projection and nested buckets) give the oracle's result bit for bit."""
+    rng = np.random.default_rng(window)
+    rows = clustered(rng, 20000, 16, 300, 0.05)
+    engine.load_rows(rows)
+    engine.set_option("hyperplane_window", window)
+    try:
+        trace, counter, _ = engine.cluster(0.8, 40, 2000, 31, 5)
+    finally:
+        engine.set_option("hyperplane_window", 0)
+    o_rows, o_off, o_ids, o_trace, o_counter = oracle.cluster(rows, 0.8, 40, 2000, 31, 5)
+    assert np.array_equal(trace, o_trace)
+    assert counter == o_counter
+    assert_same_result(engine.result(), o_rows, o_off, o_ids)
+
+
 def test_cluster_repeat_and_restore_deterministic(engine):
     rng = np.random.default_rng(5)
     rows = clustered(rng, 100000, 64, 2000, 0.05)

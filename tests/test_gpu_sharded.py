@@ -193,3 +193,39 @@ def test_rccl_single_rank_group_vs_single(engine):
         assert_same([(trace, counter, st)], eng.result(), *ref)
     finally:
         eng.close()
+
+
+def test_sharded_failure_aborts_the_group():
+    """A rank that fails (here: nothing loaded) aborts the group: the other rank's collectives
+    return an error instead of waiting for it forever, and the group stays unusable."""
+    from kmerlsh_amd import _native
+
+    rng = np.random.default_rng(5)
+    rows = clustered(rng, 20000, 16, 500, 0.05)
+    engines = [_native.Engine(0) for _ in range(2)]
+    try:
+        engines[0].load_rows(rows)
+        for e in engines:
+            e.set_option("shard_min_rows", 0)
+        _native.comm_init_local(engines)
+        errs = [None, None]
+
+        def work(r):
+            try:
+                engines[r].cluster(0.8, 5, 1000000, 3, 0)
+            except _native.KlshError as ex:
+                errs[r] = str(ex)
+
+        ts = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        assert not any(t.is_alive() for t in ts), "a rank hung after its peer failed"
+        assert errs[1] and "before a load" in errs[1]
+        assert errs[0] and "abort" in errs[0]
+        with pytest.raises(_native.KlshError, match="aborted"):
+            engines[0].cluster(0.8, 5, 1000000, 3, 0)
+    finally:
+        for e in engines:
+            e.close()
