@@ -150,6 +150,56 @@ int klsh_hyperplanes(uint32_t seed_base, uint64_t* rng_counter, int h, int d, fl
 int klsh_fp_selftest(klsh_ctx* ctx, const float* a, const float* b, uint64_t n, float* sqrt_out,
                      float* div_out);
 
+/* ---- mode E: differential k-mers and read extraction (reference app/kmerLSH.cc:521-580) ------- */
+/* AB::WRS (reference function/funcAB.cc:73-109) for every cluster at once: a cluster with more than
+ * size_thresh members (member_counts[c]) is tested with ALGLIB's pooled two-sample Student t-test
+ * (alglib::studentttest2, utils/alglib-3.15.0/src/statistics.cpp:12502) of its centroid's first n1
+ * values against the next n2 (centroids: n_clusters x (n1+n2) fp32, taken as double).
+ * group[c] = 2 if lefttail <= pvalue_thresh (its ids go to group B's k-mers), else 1 if
+ * righttail <= pvalue_thresh (group A), else 0.  Host computation, no device needed. */
+int klsh_wrs(const float* centroids, uint64_t n_clusters, int n1, int n2,
+             const uint64_t* member_counts, float pvalue_thresh, int size_thresh, uint8_t* group);
+/* The test itself: alglib::studentttest2(x, n, y, m) -> both / left / right tails (bit-exact). */
+int klsh_ttest2(const double* x, int64_t n, const double* y, int64_t m, double* bothtails,
+                double* lefttail, double* righttail);
+
+/* FASTQ records as the reference reads them (utils/fastq.cc FastqFile + kmer/kseq.h:153-200, gzip or
+ * plain): the name is the whole header line, the sequence its isgraph() characters, the quality
+ * the next len characters in [33,127].  klsh_fastq_next reads up to max_reads records into
+ * reader-owned buffers valid until the next call (offset arrays have count+1 entries) and returns
+ * the count; 0 = end of file (a truncated record ends the file, as in the reference). */
+typedef struct klsh_fastq klsh_fastq;
+klsh_fastq* klsh_fastq_open(const char* path, int* err);
+int64_t klsh_fastq_next(klsh_fastq* f, uint64_t max_reads, const char** seq,
+                        const uint64_t** seq_offsets, const char** name,
+                        const uint64_t** name_offsets, const char** qual,
+                        const uint64_t** qual_offsets);
+void klsh_fastq_close(klsh_fastq* f);
+
+/* A differential k-mer set on the context's device (the reference's uset_t, hash/HashTables.h:20):
+ * kmers are the 8-byte images of Kmer objects as kmer_set.hex stores them (kmer/Kmer.cc:307),
+ * read as little-endian uint64 (base i at bits 2i..2i+1, A/C/G/T = 0..3). */
+typedef struct klsh_kset klsh_kset;
+klsh_kset* klsh_kset_create(klsh_ctx* ctx, const uint64_t* kmers, uint64_t n, int* err);
+void klsh_kset_destroy(klsh_kset* set);
+/* IOFQ::CheckRead (reference io/ioFastQ.cc:5-76) on the GPU: read r = seq[read_offsets[r] ..
+ * read_offsets[r+1]); hits[r] (may be NULL) = k-mer positions whose canonical k-mer is in the set,
+ * flags[r] = 1 iff the read has at least k+10 bases and hits / (len-k+1) > kmer_vote (float). */
+int klsh_check_reads(klsh_ctx* ctx, const klsh_kset* set, const char* seq,
+                     const uint64_t* read_offsets, uint64_t n_reads, int k, float kmer_vote,
+                     uint32_t* hits, uint8_t* flags);
+typedef struct klsh_extract_stats {
+  uint64_t reads, bases, reads_tested, kmers_checked, reads_extracted, abnormal;
+  double kernel_ms;  /* HIP-event time of the k-mer vote kernels */
+  double parse_ms;   /* host FASTQ parsing (gzip included) */
+  double total_ms;
+} klsh_extract_stats;
+/* IOFQ::ReadExtract (reference io/ioFastQ.cc:78-159) for one sample: every record of in_path whose
+ * k-mer vote passes, written to out_path as "@name\nseq\n+\nqual\n" (plain text, byte-identical to
+ * the reference's output).  stats may be NULL. */
+int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* set, const char* in_path,
+                       const char* out_path, int k, float kmer_vote, klsh_extract_stats* stats);
+
 /* ---- synthetic workload (klsh-synth v1) ------------------------------------ */
 /* Host-side, deterministic on any machine (integer hashing + glibc exp/log/sqrt): fills counts
  * (sample-major d x n uint16, the kmer_count.bin layout) and coverage[d] = sum over i of ln(c)

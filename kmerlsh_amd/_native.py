@@ -32,7 +32,9 @@ EXPORTED = (
     "klsh_load_counts", "klsh_snapshot", "klsh_restore", "klsh_cluster", "klsh_count",
     "klsh_result", "klsh_hash_keys", "klsh_bucket_sort", "klsh_pcluster", "klsh_hyperplanes", "klsh_fp_selftest",
     "klsh_synth_counts", "klsh_comm_unique_id", "klsh_comm_init", "klsh_comm_init_local",
-    "klsh_comm_info", "klsh_set_option",
+    "klsh_comm_info", "klsh_set_option", "klsh_wrs", "klsh_ttest2", "klsh_fastq_open",
+    "klsh_fastq_next", "klsh_fastq_close", "klsh_kset_create", "klsh_kset_destroy",
+    "klsh_check_reads", "klsh_extract_fastq",
 )
 
 
@@ -58,6 +60,23 @@ class KlshStats(ctypes.Structure):
         ("small_launches", ctypes.c_uint64),
         ("small_rows", ctypes.c_uint64),
         ("small_iter_merges", ctypes.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class KlshExtractStats(ctypes.Structure):
+    _fields_ = [
+        ("reads", ctypes.c_uint64),
+        ("bases", ctypes.c_uint64),
+        ("reads_tested", ctypes.c_uint64),
+        ("kmers_checked", ctypes.c_uint64),
+        ("reads_extracted", ctypes.c_uint64),
+        ("abnormal", ctypes.c_uint64),
+        ("kernel_ms", ctypes.c_double),
+        ("parse_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -114,6 +133,18 @@ def load_library() -> ctypes.CDLL:
         "klsh_comm_info": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int),
                                           ctypes.POINTER(ctypes.c_int)]),
         "klsh_set_option": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int64]),
+        "klsh_wrs": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _P,
+                                    ctypes.c_float, ctypes.c_int, _P]),
+        "klsh_ttest2": (ctypes.c_int, [_P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P, _P]),
+        "klsh_fastq_open": (_P, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+        "klsh_fastq_next": (ctypes.c_int64, [_P, ctypes.c_uint64] + [ctypes.POINTER(_P)] * 6),
+        "klsh_fastq_close": (None, [_P]),
+        "klsh_kset_create": (_P, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]),
+        "klsh_kset_destroy": (None, [_P]),
+        "klsh_check_reads": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint64, ctypes.c_int,
+                                            ctypes.c_float, _P, _P]),
+        "klsh_extract_fastq": (ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_char_p,
+                                              ctypes.c_int, ctypes.c_float, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -165,6 +196,107 @@ def synth_counts(n: int, d: int, seed: int, genomes: int = 0, threads: int = 0):
     _check(lib.klsh_synth_counts(n, d, seed, genomes, threads, _ptr(counts), _ptr(cov)),
            "klsh_synth_counts")
     return counts, cov
+
+
+def ttest2(x: np.ndarray, y: np.ndarray) -> tuple[float, float, float]:
+    """alglib::studentttest2 as AB::WRS calls it (host restatement): (both, left, right) tails."""
+    lib = load_library()
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    out = np.zeros(3, np.float64)
+    base = out.ctypes.data
+    _check(lib.klsh_ttest2(_ptr(x), x.size, _ptr(y), y.size, base, base + 8, base + 16),
+           "klsh_ttest2")
+    return float(out[0]), float(out[1]), float(out[2])
+
+
+def wrs(centroids: np.ndarray, member_counts: np.ndarray, n1: int, n2: int, pvalue_thresh: float,
+        size_thresh: int) -> np.ndarray:
+    """AB::WRS over every cluster (host): uint8 group per cluster, 1 = group A, 2 = group B."""
+    lib = load_library()
+    c = np.ascontiguousarray(centroids, np.float32).reshape(-1, n1 + n2) if n1 + n2 else \
+        np.zeros((len(member_counts), 0), np.float32)
+    mc = np.ascontiguousarray(member_counts, np.uint64)
+    g = np.zeros(mc.size, np.uint8)
+    _check(lib.klsh_wrs(_ptr(c), mc.size, n1, n2, _ptr(mc), ctypes.c_float(pvalue_thresh),
+                        int(size_thresh), _ptr(g)), "klsh_wrs")
+    return g
+
+
+def fastq_records(path: str, batch: int = 1 << 16):
+    """Every record of a FASTQ(.gz) as the reference's FastqFile/kseq reads it (host):
+    a list of (name, seq, qual) byte strings."""
+    lib = load_library()
+    err = ctypes.c_int(0)
+    f = lib.klsh_fastq_open(path.encode(), ctypes.byref(err))
+    if not f:
+        _check(err.value or -1, "klsh_fastq_open")
+    out = []
+    try:
+        while True:
+            ptrs = [_P() for _ in range(6)]
+            n = lib.klsh_fastq_next(f, batch, *[ctypes.byref(p) for p in ptrs])
+            if n < 0:
+                _check(int(n), "klsh_fastq_next")
+            if n == 0:
+                break
+            offs = [np.ctypeslib.as_array(ctypes.cast(ptrs[i], ctypes.POINTER(ctypes.c_uint64)),
+                                          shape=(n + 1,)).copy() for i in (1, 3, 5)]
+            blobs = [ctypes.string_at(ptrs[i], int(o[-1])) if o[-1] else b""
+                     for i, o in zip((0, 2, 4), offs)]
+            so, no, qo = offs
+            sb, nb, qb = blobs
+            for r in range(n):
+                out.append((nb[no[r]:no[r + 1]], sb[so[r]:so[r + 1]], qb[qo[r]:qo[r + 1]]))
+    finally:
+        lib.klsh_fastq_close(f)
+    return out
+
+
+class KmerSet:
+    """A differential k-mer set on an Engine's device (``klsh_kset``)."""
+
+    def __init__(self, engine: "Engine", kmers: np.ndarray):
+        self._lib = engine._lib
+        self.engine = engine
+        k = np.ascontiguousarray(kmers, np.uint64)
+        err = ctypes.c_int(0)
+        self._set = self._lib.klsh_kset_create(engine._ctx, _ptr(k), k.size, ctypes.byref(err))
+        if not self._set:
+            _check(err.value or -2, "klsh_kset_create")
+        self.size = k.size
+
+    def close(self) -> None:
+        if getattr(self, "_set", None):
+            self._lib.klsh_kset_destroy(self._set)
+            self._set = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check_reads(self, seqs, k: int, kmer_vote: float):
+        """IOFQ::CheckRead on the GPU: (hits uint32, flags uint8) per read (bytes sequences)."""
+        blob = b"".join(seqs)
+        off = np.zeros(len(seqs) + 1, np.uint64)
+        off[1:] = np.cumsum([len(s) for s in seqs], dtype=np.uint64)
+        buf = np.frombuffer(blob + b"\0", np.uint8)
+        hits = np.zeros(len(seqs), np.uint32)
+        flags = np.zeros(len(seqs), np.uint8)
+        _check(self._lib.klsh_check_reads(self.engine._ctx, self._set, _ptr(buf), _ptr(off),
+                                          len(seqs), k, ctypes.c_float(kmer_vote), _ptr(hits),
+                                          _ptr(flags)), "klsh_check_reads")
+        return hits, flags
+
+    def extract_fastq(self, in_path: str, out_path: str, k: int, kmer_vote: float) -> dict:
+        """IOFQ::ReadExtract for one sample (host parse + GPU vote + writer)."""
+        st = KlshExtractStats()
+        _check(self._lib.klsh_extract_fastq(self.engine._ctx, self._set, in_path.encode(),
+                                            out_path.encode(), k, ctypes.c_float(kmer_vote),
+                                            ctypes.byref(st)), "klsh_extract_fastq")
+        return st.as_dict()
 
 
 class Engine:

@@ -1,11 +1,18 @@
-// kmerLSH-compatible command line (mode C) over the gfx950 engine.
+// kmerLSH-compatible command line (modes C and E) over the gfx950 engine.
 //
-// Same flags and files as the reference (app/kmerLSH.cc:147-276, :432-520): run in the directory
-// holding kmer_count.bin / kmer_count.log, with -a/-b sample lists; writes
-// <F>.clust ("<n>\t<id>\t...\n" per cluster with more than 5 members, io/ioMatrix.cc:265-294)
-// and <F> (raw fp32 centroids of the same clusters, io/ioMatrix.cc:322-351).
-//   kmerLSH -a A.txt -b B.txt [-I iters] [-N min_sim] [-F file] [-M C --only] [--verbose]
-//           [--seed S] [--device D]
+// Same flags and files as the reference (app/kmerLSH.cc:147-276, :432-580), run in the directory
+// holding kmer_count.bin / kmer_count.log, with -a/-b sample lists ("<fastq> <kmc name>" lines):
+//   mode C  writes <F>.clust ("<n>\t<id>\t...\n" per cluster with more than 5 members,
+//           io/ioMatrix.cc:265-294) and <F> (raw fp32 centroids of the same clusters, :322-351);
+//   mode E  reads <F> / <F>.clust back (io/ioMatrix.cc:48-119), tests every cluster with more than
+//           -S members (AB::WRS, function/funcAB.cc:73-109), builds the two differential k-mer
+//           sets from kmer_set.hex on the GPU and writes <o>_<sample> / <p>_<sample>: the reads
+//           whose k-mer vote passes -V (IOFQ::Extracting, io/ioFastQ.cc:161-195).
+// Mode selection as the reference's (app/kmerLSH.cc:234-275): -M E [--only] extracts only,
+// -M C --only clusters only, -M C clusters and then extracts; modes K and B (KMC3 counting) are
+// not part of this engine.
+//   kmerLSH -a A.txt -b B.txt [-o A -p B] [-I iters] [-N min_sim] [-K k] [-S size] [-P pval]
+//           [-V vote] [-F file] [-M C|E] [--only] [--verbose] [--seed S] [--device D]
 // Additions: --seed (the reference seeds from std::random_device; SURVEY.md §8(c) convention)
 // and --device.  -T is accepted and ignored (results never depend on a thread count).
 // The init pass keeps the reference's 1e8-row batching and re-cluster passes
@@ -14,6 +21,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <ctype.h>
 
 #include <chrono>
 #include <string>
@@ -98,18 +106,179 @@ char* put_u64(char* p, uint64_t v) {
   return p;
 }
 
+// GetInput (io/ioHT.cc:3-19): the first token of every line (std::getline) of a sample list
+std::vector<std::string> sample_paths(const char* path) {
+  std::vector<std::string> out;
+  FILE* f = fopen(path, "rb");
+  if (!f) {
+    fprintf(stderr, "Unable to open info file");
+    return out;
+  }
+  std::string line;
+  int c;
+  bool any = false;
+  auto flush = [&]() {
+    size_t a = 0;
+    while (a < line.size() && isspace((unsigned char)line[a])) ++a;
+    size_t b = a;
+    while (b < line.size() && !isspace((unsigned char)line[b])) ++b;
+    out.push_back(line.substr(a, b - a));
+    line.clear();
+  };
+  while ((c = fgetc(f)) != EOF) {
+    any = true;
+    if (c == '\n') flush();
+    else line.push_back((char)c);
+  }
+  if (any && !line.empty()) flush();
+  fclose(f);
+  return out;
+}
+
+// Mode E (app/kmerLSH.cc:521-580).
+int run_extract(klsh_ctx* ctx, const std::vector<std::string>& s1,
+                const std::vector<std::string>& s2, const std::string& clust_file,
+                const std::string& out1, const std::string& out2, int k, int size_thresh,
+                float pval, float vote, bool verbose) {
+  const int n1 = (int)s1.size(), n2 = (int)s2.size(), d = n1 + n2;
+  if (verbose) printf("Start to extract the differential reads from raw data\n");
+  // IOMat::ReadClusterAll: centroid rows of <F>, member lists of <F>.clust, paired line by line
+  FILE* fb = fopen(clust_file.c_str(), "rb");
+  if (!fb) {
+    printf("Error! file ( %s ) not open!\n", clust_file.c_str());
+    return 1;
+  }
+  fseek(fb, 0, SEEK_END);
+  const uint64_t line_cnt = d > 0 ? (uint64_t)ftell(fb) / (sizeof(float) * d) : 0;
+  fseek(fb, 0, SEEK_SET);
+  std::vector<float> values(line_cnt * (uint64_t)d);
+  if (line_cnt && fread(values.data(), sizeof(float) * d, line_cnt, fb) != line_cnt) {
+    fprintf(stderr, "kmerLSH: short read of %s\n", clust_file.c_str());
+    return 1;
+  }
+  fclose(fb);
+  const std::string cf = clust_file + ".clust";
+  FILE* fc = fopen(cf.c_str(), "rb");
+  if (!fc) {
+    printf("Error! file ( %s ) not open!\n", cf.c_str());
+    return 1;
+  }
+  std::vector<uint64_t> counts, ids, off{0};
+  {
+    std::string line;
+    int c;
+    auto parse = [&]() {  // strtol chain: n, then up to n ids, missing ones stay 0
+      const char* p = line.c_str();
+      char* e = nullptr;
+      const uint64_t n = (uint64_t)strtol(p, &e, 10);
+      uint64_t got = 0;
+      std::vector<uint64_t> v(n, 0);
+      while (p != e && got < n) {
+        p = e;
+        v[got++] = (uint64_t)strtol(p, &e, 10);
+      }
+      counts.push_back(n);
+      ids.insert(ids.end(), v.begin(), v.end());
+      off.push_back(ids.size());
+      line.clear();
+    };
+    bool any = false;
+    while ((c = fgetc(fc)) != EOF) {
+      any = true;
+      if (c == '\n') parse();
+      else line.push_back((char)c);
+    }
+    if (any && !line.empty()) parse();
+    fclose(fc);
+  }
+  if (counts.size() != line_cnt) {
+    fprintf(stderr, "kmerLSH: %s has %zu clusters, %s %llu rows (the reference requires equal)\n",
+            cf.c_str(), counts.size(), clust_file.c_str(), (unsigned long long)line_cnt);
+    return 1;
+  }
+  std::vector<uint8_t> group(line_cnt);
+  check(klsh_wrs(values.data(), line_cnt, n1, n2, counts.data(), pval, size_thresh, group.data()),
+        "klsh_wrs");
+  // kmer_count.log: kmap_size; kmer_set.hex: kmap_size k-mers of 8 bytes (Kmer::writeBytes)
+  FILE* lf = fopen("kmer_count.log", "r");
+  unsigned long long kmap = 0;
+  if (!lf || fscanf(lf, "%llu", &kmap) != 1) {
+    fprintf(stderr, "kmerLSH: kmer_count.log unreadable\n");
+    return 1;
+  }
+  fclose(lf);
+  // distinct ids per group (the reference's two unordered_sets); a k-mer goes to A if its id is in
+  // A's set, else to B if in B's (app/kmerLSH.cc:565-571)
+  std::vector<uint8_t> in1(kmap, 0), in2(kmap, 0);
+  uint64_t na = 0, nb = 0;
+  for (uint64_t c = 0; c < line_cnt; ++c)
+    for (uint64_t q = off[c]; q < off[c + 1]; ++q) {
+      if (ids[q] >= kmap) continue;
+      if (group[c] == 1 && !in1[ids[q]]) in1[ids[q]] = 1, na += 1;
+      if (group[c] == 2 && !in2[ids[q]]) in2[ids[q]] = 1, nb += 1;
+    }
+  if (verbose) {
+    printf("# of differential kmers in group A : %llu\n", (unsigned long long)na);
+    printf("# of differential kmers in group B : %llu\n", (unsigned long long)nb);
+  }
+  std::vector<uint64_t> kmers(kmap), k1, k2;
+  FILE* kf = fopen("kmer_set.hex", "rb");
+  if (!kf || fread(kmers.data(), 8, kmap, kf) != kmap) {
+    fprintf(stderr, "kmerLSH: kmer_set.hex unreadable\n");
+    return 1;
+  }
+  fclose(kf);
+  for (uint64_t i = 0; i < kmap; ++i) {
+    if (in1[i]) k1.push_back(kmers[i]);
+    else if (in2[i]) k2.push_back(kmers[i]);
+  }
+  int err = 0;
+  klsh_kset* set1 = klsh_kset_create(ctx, k1.data(), k1.size(), &err);
+  check(err, "klsh_kset_create");
+  klsh_kset* set2 = klsh_kset_create(ctx, k2.data(), k2.size(), &err);
+  check(err, "klsh_kset_create");
+  for (int g = 0; g < 2; ++g) {  // IOFQ::Extracting per group
+    const auto& ss = g == 0 ? s1 : s2;
+    const std::string& pre = g == 0 ? out1 : out2;
+    if (verbose) printf("start %d threads\n", 1);
+    for (const std::string& path : ss) {
+      const size_t slash = path.find_last_of('/');
+      const std::string base = slash == std::string::npos ? path : path.substr(slash + 1);
+      const std::string out = pre + "_" + base;
+      if (verbose) printf("writing to %s\n", out.c_str());
+      fflush(stdout);
+      klsh_extract_stats st;
+      check(klsh_extract_fastq(ctx, g == 0 ? set1 : set2, path.c_str(), out.c_str(), k, vote, &st),
+            "klsh_extract_fastq");
+      if (verbose)
+        printf("  %llu reads, %llu extracted; k-mer vote kernel %.3f ms, parse %.3f ms\n",
+               (unsigned long long)st.reads, (unsigned long long)st.reads_extracted, st.kernel_ms,
+               st.parse_ms);
+    }
+  }
+  klsh_kset_destroy(set1);
+  klsh_kset_destroy(set2);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   const char *in1 = nullptr, *in2 = nullptr;
-  std::string out = "clustering_result.txt", mode;
-  int iters = 100, verbose = 0, only = 0, device = 0;
-  float min_sim = 0.80f;
+  std::string out = "clustering_result.txt", mode, out1, out2;
+  int iters = 100, verbose = 0, only = 0, device = 0, kmer_k = 23, size_thresh = 500000;
+  float min_sim = 0.80f, pval = 0.01f, vote = 0.5f;
   uint32_t seed = 12345u;
   static struct option lo[] = {{"verbose", no_argument, 0, 1},
                                {"only", no_argument, 0, 2},
                                {"seed", required_argument, 0, 3},
                                {"device", required_argument, 0, 4},
+                               {"output1", required_argument, 0, 'o'},
+                               {"output2", required_argument, 0, 'p'},
+                               {"kmer_size", required_argument, 0, 'K'},
+                               {"size_thresh", required_argument, 0, 'S'},
+                               {"pval_thresh", required_argument, 0, 'P'},
+                               {"kmer_vote", required_argument, 0, 'V'},
                                {"input1", required_argument, 0, 'a'},
                                {"input2", required_argument, 0, 'b'},
                                {"cluster_iteration", required_argument, 0, 'I'},
@@ -125,6 +294,12 @@ int main(int argc, char** argv) {
       case 2: only = 1; break;
       case 3: seed = (uint32_t)strtoul(optarg, nullptr, 10); break;
       case 4: device = atoi(optarg); break;
+      case 'o': out1 = optarg; break;
+      case 'p': out2 = optarg; break;
+      case 'K': kmer_k = atoi(optarg); break;
+      case 'S': size_thresh = atoi(optarg); break;
+      case 'P': pval = (float)atof(optarg); break;
+      case 'V': vote = (float)atof(optarg); break;
       case 'a': in1 = optarg; break;
       case 'b': in2 = optarg; break;
       case 'I': iters = atoi(optarg); break;
@@ -135,16 +310,33 @@ int main(int argc, char** argv) {
     }
   }
   if (argc < 2 || !in1 || !in2) {
-    fprintf(stderr, "usage: kmerLSH -a A.txt -b B.txt [-I iters] [-N min_sim] [-F out] [-M C --only]\n");
+    fprintf(stderr, "usage: kmerLSH -a A.txt -b B.txt [-o A -p B] [-I iters] [-N min_sim] [-K k] "
+                    "[-S size] [-P pval] [-V vote] [-F out] [-M C|E] [--only]\n");
     return 1;
   }
-  if (!mode.empty() && mode != "C") {
-    fprintf(stderr, "kmerLSH (gfx950): only mode C (clustering) is implemented\n");
+  if (mode != "C" && mode != "E") {
+    fprintf(stderr, "kmerLSH (gfx950): modes C (clustering) and E (extraction) are implemented; "
+                    "K / B (KMC3 counting, kmer_count.bin) are not: pass -M C or -M E\n");
     return 1;
   }
-  (void)only;
+  const bool clustering = mode == "C", extracting = mode == "E" || !only;
   const auto t0 = std::chrono::steady_clock::now();
   const int d = count_lines(in1) + count_lines(in2);
+  if (!clustering) {
+    int err = 0;
+    klsh_ctx* ctx = klsh_create(device, &err);
+    if (!ctx) {
+      fprintf(stderr, "kmerLSH: %s\n", klsh_last_error());
+      return 2;
+    }
+    const int rc = run_extract(ctx, sample_paths(in1), sample_paths(in2), out, out1, out2, kmer_k,
+                               size_thresh, pval, vote, verbose);
+    klsh_destroy(ctx);
+    const double secs =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (verbose) printf("extracting reads takes (secs): %g\n", secs);
+    return rc;
+  }
 
   FILE* lf = fopen("kmer_count.log", "r");
   if (!lf) {
@@ -216,7 +408,6 @@ int main(int argc, char** argv) {
   RowSet fin;
   fin.d = d;
   fetch(ctx, d, &fin);
-  klsh_destroy(ctx);
 
   // SaveResult / SaveBinary, ignore_small = 5 (app/kmerLSH.cc:498-499)
   const std::string clust = out + ".clust";
@@ -248,9 +439,14 @@ int main(int argc, char** argv) {
   fwrite(buf.data(), 1, p - buf.data(), fc);
   fclose(fc);
   fclose(fb);
+  int rc = 0;
+  if (extracting)
+    rc = run_extract(ctx, sample_paths(in1), sample_paths(in2), out, out1, out2, kmer_k,
+                     size_thresh, pval, vote, verbose);
+  klsh_destroy(ctx);
   const double secs =
       std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   printf("kmerLSH (gfx950) in total takes (secs): %g, clusters: %llu\n", secs,
          (unsigned long long)fin.n());
-  return 0;
+  return rc;
 }

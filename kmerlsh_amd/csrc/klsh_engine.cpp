@@ -440,6 +440,12 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 
 }  // namespace
 
+namespace klsh {
+int ctx_device(const klsh_ctx* ctx) { return ctx->device; }
+hipStream_t ctx_stream(const klsh_ctx* ctx) { return ctx->stream; }
+int set_error(int code, const char* msg) { return fail(code, msg); }
+}  // namespace klsh
+
 // ===================================================================================== C ABI ===
 extern "C" {
 

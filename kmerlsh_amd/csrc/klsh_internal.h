@@ -6,6 +6,8 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include "klsh.h"
+
 namespace klsh {
 
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;  // dead position marker in a bucket's slot run
@@ -232,5 +234,20 @@ void merge_prof_dump(FILE* f);
 
 // a[i] = min(a[i], b[i])
 void launch_min_u32(uint32_t* a, const uint32_t* b, size_t n, hipStream_t s);
+
+// ---- mode E (klsh_extract.hip): differential k-mer sets and the per-read k-mer vote ----------
+// tab: `mask + 1` (a power of two) 64-bit slots, all ones = empty; kmers[i] == all ones skipped.
+void launch_kset_insert(const uint64_t* kmers, uint64_t n, uint64_t* tab, uint64_t mask,
+                        hipStream_t s);
+// Read r = seq[off[r] .. off[r+1]): hits[r] = its k-mer positions whose canonical k-mer is in the
+// set, flags[r] = hits / (len - k + 1) > vote (float), both 0 for reads shorter than k + 10.
+void launch_check_reads(const uint8_t* seq, const uint64_t* off, uint64_t n, int k, float vote,
+                        const uint64_t* tab, uint64_t mask, uint32_t* hits, uint8_t* flags,
+                        hipStream_t s);
+
+// The engine's context, for the other host translation units (klsh_extract.cpp).
+int ctx_device(const klsh_ctx* ctx);
+hipStream_t ctx_stream(const klsh_ctx* ctx);
+int set_error(int code, const char* msg);  // sets klsh_last_error(), returns code
 
 }  // namespace klsh

@@ -12,6 +12,8 @@
 //   Utility::IOMat::ReadClusterAll      io/ioMatrix.cc:48
 //   Utility::IOMat::SaveResult / SaveBinary   io/ioMatrix.cc:265 / :322
 //   Utility::IOMat::convertHTMat        io/ioMatrix.cc:353
+//   alglib::studentttest2               utils/alglib-3.15.0/src/statistics.cpp:12502 (AB::WRS's test,
+//                                       function/funcAB.cc:100)
 //
 // Run with OMP_THREAD_LIMIT=1 (T=1 semantics) and KLSH_SEED=<seed> (ref_seed.cc).
 #include <cstdint>
@@ -23,6 +25,7 @@
 
 #include "function/cluster.h"
 #include "io/ioMatrix.h"
+#include "utils/alglib-3.15.0/src/statistics.h"
 
 using namespace std;
 
@@ -72,7 +75,9 @@ int main(int argc, char** argv) {
             "  ref_harness cluster ROWS N D MINSIM I BTHR OUTPREFIX\n"
             "  ref_harness cluster_from BINPREFIX D MINSIM I BTHR OUTPREFIX   (input via ReadClusterAll)\n"
             "  ref_harness cluster_w ROWS OFF IDS N D MINSIM I BTHR OUTPREFIX (binary member lists)\n"
-            "  ref_harness convert COUNTS N D VKMERS OUTPREFIX  (uint16 sample-major counts -> convertHTMat)\n");
+            "  ref_harness convert COUNTS N D VKMERS OUTPREFIX  (uint16 sample-major counts -> convertHTMat)\n"
+            "  ref_harness ttest VALUES N M COUNT OUT       (f32 cases of N+M values -> studentttest2,\n"
+            "                                               f64 bothtails/lefttail/righttail per case)\n");
     return 1;
   }
   const string cmd = argv[1];
@@ -199,6 +204,27 @@ int main(int argc, char** argv) {
     vector<Abundance*> v;
     IOMat::convertHTMat(ary.data(), v_kmers, d, false, n, 0, &v);
     save(&v, argv[6]);
+    return 0;
+  }
+  if (cmd == "ttest") {  // the values as AB::WRS passes them: float -> double (funcAB.cc:88-93)
+    const int n = atoi(argv[3]), m = atoi(argv[4]);
+    const size_t count = strtoull(argv[5], nullptr, 10);
+    vector<float> v = read_f32(argv[2], count * (size_t)(n + m));
+    vector<double> out(3 * count);
+    for (size_t c = 0; c < count; ++c) {
+      vector<double> x(n > 0 ? n : 1), y(m > 0 ? m : 1);
+      for (int i = 0; i < n; ++i) x[i] = (double)v[c * (n + m) + i];
+      for (int j = 0; j < m; ++j) y[j] = (double)v[c * (n + m) + n + j];
+      alglib::real_1d_array ax, ay;
+      ax.setcontent(n, x.data());
+      ay.setcontent(m, y.data());
+      double both = 0, left = 0, right = 0;
+      alglib::studentttest2(ax, n, ay, m, both, left, right);
+      out[3 * c] = both;
+      out[3 * c + 1] = left;
+      out[3 * c + 2] = right;
+    }
+    write_bytes(argv[6], out.data(), out.size() * 8);
     return 0;
   }
   fprintf(stderr, "unknown command %s\n", cmd.c_str());
