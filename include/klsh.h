@@ -200,6 +200,22 @@ typedef struct klsh_extract_stats {
 int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* set, const char* in_path,
                        const char* out_path, int k, float kmer_vote, klsh_extract_stats* stats);
 
+/* ---- mode B: the k-mer table of KMC databases (reference io/ioHT.cc:83-199, kmc = false) ------- */
+/* buildKHtable over KMC databases (KMC1 or KMC2/3 layout, <name>.kmc_pre / <name>.kmc_suf, listing
+ * as kmer/kmc_api/kmc_file.cpp:66-532): the union of canonical k-mers over the samples, each
+ * sample's summed counts clamped at 65535, written to <out_dir>/ kmer_set.hex (8 bytes per k-mer),
+ * kmer_count.bin (sample-major uint16) and kmer_count.log ("%llu" rows, "\t%f" coverage = float sum
+ * of log(count) per sample).  The rows, counts and log equal the reference's; the reference's row
+ * ORDER is its hash table's (libcuckoo), here it is first appearance (sample, then file order).
+ * out_dir NULL or "" = the current directory.  stats may be NULL. */
+typedef struct klsh_khtable_stats {
+  uint64_t kmap_size, records, records_listed;
+  double io_ms;     /* host reads of the .kmc_suf streams */
+  double total_ms;
+} klsh_khtable_stats;
+int klsh_build_khtable(klsh_ctx* ctx, const char* const* kmc_names, int n_samples, int k,
+                       const char* out_dir, klsh_khtable_stats* stats);
+
 /* ---- synthetic workload (klsh-synth v1) ------------------------------------ */
 /* Host-side, deterministic on any machine (integer hashing + glibc exp/log/sqrt): fills counts
  * (sample-major d x n uint16, the kmer_count.bin layout) and coverage[d] = sum over i of ln(c)

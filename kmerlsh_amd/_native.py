@@ -34,7 +34,7 @@ EXPORTED = (
     "klsh_synth_counts", "klsh_comm_unique_id", "klsh_comm_init", "klsh_comm_init_local",
     "klsh_comm_info", "klsh_set_option", "klsh_wrs", "klsh_ttest2", "klsh_fastq_open",
     "klsh_fastq_next", "klsh_fastq_close", "klsh_kset_create", "klsh_kset_destroy",
-    "klsh_check_reads", "klsh_extract_fastq",
+    "klsh_check_reads", "klsh_extract_fastq", "klsh_build_khtable",
 )
 
 
@@ -76,6 +76,19 @@ class KlshExtractStats(ctypes.Structure):
         ("abnormal", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_double),
         ("parse_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class KlshKhtableStats(ctypes.Structure):
+    _fields_ = [
+        ("kmap_size", ctypes.c_uint64),
+        ("records", ctypes.c_uint64),
+        ("records_listed", ctypes.c_uint64),
+        ("io_ms", ctypes.c_double),
         ("total_ms", ctypes.c_double),
     ]
 
@@ -145,6 +158,8 @@ def load_library() -> ctypes.CDLL:
                                             ctypes.c_float, _P, _P]),
         "klsh_extract_fastq": (ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_char_p,
                                               ctypes.c_int, ctypes.c_float, _P]),
+        "klsh_build_khtable": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_char_p, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -383,6 +398,14 @@ class Engine:
                                       bucket_size_threshold, seed, ctypes.byref(c), _ptr(trace),
                                       ctypes.byref(st)), "klsh_cluster")
         return trace[: st.iterations], c.value, st.as_dict()
+
+    def build_khtable(self, kmc_names, k: int, out_dir: str = "") -> dict:
+        """Mode B: kmer_set.hex / kmer_count.bin / kmer_count.log from KMC databases."""
+        arr = (ctypes.c_char_p * len(kmc_names))(*[n.encode() for n in kmc_names])
+        st = KlshKhtableStats()
+        _check(self._lib.klsh_build_khtable(self._ctx, arr, len(kmc_names), k, out_dir.encode(),
+                                            ctypes.byref(st)), "klsh_build_khtable")
+        return st.as_dict()
 
     def pcluster(self, thr: float) -> None:
         _check(self._lib.klsh_pcluster(self._ctx, ctypes.c_float(thr)), "klsh_pcluster")

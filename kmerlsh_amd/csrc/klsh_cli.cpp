@@ -8,9 +8,12 @@
 //           -S members (AB::WRS, function/funcAB.cc:73-109), builds the two differential k-mer
 //           sets from kmer_set.hex on the GPU and writes <o>_<sample> / <p>_<sample>: the reads
 //           whose k-mer vote passes -V (IOFQ::Extracting, io/ioFastQ.cc:161-195).
+//   mode B  reads the KMC databases named in the lists' second column and writes kmer_set.hex,
+//           kmer_count.bin, kmer_count.log (io/ioHT.cc:83-199 with existing databases).
 // Mode selection as the reference's (app/kmerLSH.cc:234-275): -M E [--only] extracts only,
-// -M C --only clusters only, -M C clusters and then extracts; modes K and B (KMC3 counting) are
-// not part of this engine.
+// -M C --only clusters only, -M C clusters and then extracts, -M B --only builds the table only,
+// -M B builds, clusters and extracts; mode K (running the KMC counter itself) is not part of
+// this engine.
 //   kmerLSH -a A.txt -b B.txt [-o A -p B] [-I iters] [-N min_sim] [-K k] [-S size] [-P pval]
 //           [-V vote] [-F file] [-M C|E] [--only] [--verbose] [--seed S] [--device D]
 // Additions: --seed (the reference seeds from std::random_device; SURVEY.md §8(c) convention)
@@ -106,8 +109,9 @@ char* put_u64(char* p, uint64_t v) {
   return p;
 }
 
-// GetInput (io/ioHT.cc:3-19): the first token of every line (std::getline) of a sample list
-std::vector<std::string> sample_paths(const char* path) {
+// GetInput (io/ioHT.cc:3-19): token `col` (0: the sample, 1: its KMC database name) of every line
+// (std::getline) of a sample list
+std::vector<std::string> sample_paths(const char* path, int col = 0) {
   std::vector<std::string> out;
   FILE* f = fopen(path, "rb");
   if (!f) {
@@ -118,10 +122,13 @@ std::vector<std::string> sample_paths(const char* path) {
   int c;
   bool any = false;
   auto flush = [&]() {
-    size_t a = 0;
-    while (a < line.size() && isspace((unsigned char)line[a])) ++a;
-    size_t b = a;
-    while (b < line.size() && !isspace((unsigned char)line[b])) ++b;
+    size_t a = 0, b = 0;
+    for (int t = 0; t <= col; ++t) {
+      a = b;
+      while (a < line.size() && isspace((unsigned char)line[a])) ++a;
+      b = a;
+      while (b < line.size() && !isspace((unsigned char)line[b])) ++b;
+    }
     out.push_back(line.substr(a, b - a));
     line.clear();
   };
@@ -133,6 +140,22 @@ std::vector<std::string> sample_paths(const char* path) {
   if (any && !line.empty()) flush();
   fclose(f);
   return out;
+}
+
+// Mode B (buildKHtable with kmc = false, io/ioHT.cc:83-199): the KMC databases named in the sample
+// lists' second column -> kmer_set.hex / kmer_count.bin / kmer_count.log in the current directory.
+int run_build(klsh_ctx* ctx, const char* in1, const char* in2, int k, bool verbose) {
+  std::vector<std::string> names = sample_paths(in1, 1), n2 = sample_paths(in2, 1);
+  names.insert(names.end(), n2.begin(), n2.end());
+  std::vector<const char*> ptrs;
+  for (const auto& n : names) ptrs.push_back(n.c_str());
+  klsh_khtable_stats st;
+  check(klsh_build_khtable(ctx, ptrs.data(), (int)ptrs.size(), k, "", &st), "klsh_build_khtable");
+  if (verbose)
+    printf("k-mer table: %llu k-mers from %llu records of %zu databases (%.1f ms, %.1f ms reading)\n",
+           (unsigned long long)st.kmap_size, (unsigned long long)st.records, names.size(),
+           st.total_ms, st.io_ms);
+  return 0;
 }
 
 // Mode E (app/kmerLSH.cc:521-580).
@@ -314,14 +337,28 @@ int main(int argc, char** argv) {
                     "[-S size] [-P pval] [-V vote] [-F out] [-M C|E] [--only]\n");
     return 1;
   }
-  if (mode != "C" && mode != "E") {
-    fprintf(stderr, "kmerLSH (gfx950): modes C (clustering) and E (extraction) are implemented; "
-                    "K / B (KMC3 counting, kmer_count.bin) are not: pass -M C or -M E\n");
+  if (mode != "B" && mode != "C" && mode != "E") {
+    fprintf(stderr, "kmerLSH (gfx950): modes B (k-mer table from KMC databases), C (clustering) and "
+                    "E (extraction) are implemented; K (running the KMC counter) is not: count "
+                    "with KMC, then pass -M B\n");
     return 1;
   }
-  const bool clustering = mode == "C", extracting = mode == "E" || !only;
+  // app/kmerLSH.cc:234-275: --only runs the named mode; without it the later modes follow
+  const bool building = mode == "B", clustering = mode == "C" || (mode == "B" && !only);
+  const bool extracting = mode == "E" || !only;
   const auto t0 = std::chrono::steady_clock::now();
   const int d = count_lines(in1) + count_lines(in2);
+  if (building) {
+    int err = 0;
+    klsh_ctx* ctx = klsh_create(device, &err);
+    if (!ctx) {
+      fprintf(stderr, "kmerLSH: %s\n", klsh_last_error());
+      return 2;
+    }
+    const int rc = run_build(ctx, in1, in2, kmer_k, verbose);
+    klsh_destroy(ctx);
+    if (rc || (!clustering && !extracting)) return rc;
+  }
   if (!clustering) {
     int err = 0;
     klsh_ctx* ctx = klsh_create(device, &err);

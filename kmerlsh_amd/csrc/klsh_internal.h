@@ -245,6 +245,36 @@ void launch_check_reads(const uint8_t* seq, const uint64_t* off, uint64_t n, int
                         const uint64_t* tab, uint64_t mask, uint32_t* hits, uint8_t* flags,
                         hipStream_t s);
 
+// ---- mode B (klsh_kmc.hip): the k-mer table of KMC databases ---------------------------------
+struct KmcParams {
+  int k, p;                   // k-mer length, LUT prefix symbols
+  uint32_t sufix_size;        // (k - p) / 4 bytes per record
+  uint32_t counter_size;      // bytes
+  uint32_t rec_size;          // sufix_size + counter_size
+  uint32_t min_count;
+  uint64_t max_count;
+  uint64_t prefix_mask;       // (1 << 2p) - 1
+};
+// records [0, n) of a .kmc_suf chunk starting at record rec0 -> canonical rep (all ones = outside
+// [min_count, max_count]) and counter; *n_valid += records kept.  lut: lut_n entries, the last the
+// total + 1 sentinel.
+void launch_kmc_decode(const uint8_t* recs, uint64_t n, uint64_t rec0, const KmcParams& kp,
+                       const uint64_t* lut, uint64_t lut_n, uint64_t* rep, uint32_t* cnt,
+                       uint32_t* n_valid, hipStream_t s);
+void launch_kmc_union(const uint64_t* rep, uint64_t n, uint64_t ord0, uint64_t* tab,
+                      uint64_t* first, uint64_t mask, hipStream_t s);
+void launch_kmc_count(const uint64_t* rep, const uint32_t* cnt, uint64_t n, const uint64_t* tab,
+                      uint64_t mask, uint32_t* acc, hipStream_t s);
+// occupied slots -> (low word of their first-appearance ordinal, slot), *n_out of them
+void launch_kmc_collect(const uint64_t* tab, const uint64_t* first, uint64_t cap, uint32_t* lo,
+                        uint32_t* slot, uint32_t* n_out, hipStream_t s);
+void launch_kmc_hi(const uint64_t* first, const uint32_t* slots, uint64_t n, uint32_t* hi,
+                   hipStream_t s);
+void launch_kmc_emit_keys(const uint64_t* tab, const uint32_t* order, uint64_t n, uint64_t* out,
+                          hipStream_t s);
+void launch_kmc_emit(const uint32_t* acc, const uint32_t* order, uint64_t n, uint16_t* out,
+                     hipStream_t s);
+
 // The engine's context, for the other host translation units (klsh_extract.cpp).
 int ctx_device(const klsh_ctx* ctx);
 hipStream_t ctx_stream(const klsh_ctx* ctx);
