@@ -129,11 +129,21 @@ __global__ __launch_bounds__(256) void k_kmc_collect(const uint64_t* __restrict_
                                                      uint64_t cap, uint32_t* __restrict__ lo,
                                                      uint32_t* __restrict__ slot,
                                                      uint32_t* __restrict__ n_out) {
+  // cap is a power of two >= 1024: every wave's 64 lanes are in or out of range together
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * 256ull) {
-    if (tab[i] == kKmcEmpty) continue;
-    const uint32_t o = atomicAdd(n_out, 1u);
-    lo[o] = (uint32_t)first[i];
-    slot[o] = (uint32_t)i;
+    const bool occ = tab[i] != kKmcEmpty;
+    const uint64_t m = __ballot(occ);
+    if (!m) continue;
+    uint32_t base = 0;  // one add per wave, not per entry (a single counter)
+    if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(n_out, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)__builtin_ctzll(m), 64);
+    if (occ) {
+      const uint32_t o = base + (uint32_t)__popcll(m & below);
+      lo[o] = (uint32_t)first[i];
+      slot[o] = (uint32_t)i;
+    }
   }
 }
 
