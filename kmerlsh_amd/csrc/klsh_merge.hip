@@ -272,9 +272,12 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
   uint32_t size = b;
   uint32_t nmerged = 0;
   bool dirty = false;
-  if (__ballot(valid && P != 0ull)) {
+  const uint64_t matched = __ballot(valid && P != 0ull);
+  if (matched) {
     uint32_t rid = g, cnt = 0u, hd = 0u, tl = 0u;
-    if (valid) {
+    // metadata only for the runs with a matching pair: ~1 % of the rows merge per iteration, and
+    // three random 4-B reads cost a line each (as much traffic as the row itself)
+    if (valid && (matched & gmask) != 0ull) {
       cnt = r.cnt[slot];
       hd = r.head[slot];
       tl = r.tail[slot];
@@ -334,22 +337,24 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
       }
       wave_lds_fence();
       const bool need = active && g >= i && g < size;
-      if (active && g == i && i < size) load_row<D>(lds + (gbase + rid) * ST, x);
-      // decisions of the positions still to be visited against the new row at j (read from LDS
-      // 16 B at a time: the chains need no copy of it in registers)
+      // decisions of the positions still to be visited against the new row at j; both rows are
+      // read from LDS 16 B at a time (the lane's own row is its row id's: no registers held
+      // across the walk)
       const float* cr = lds + (gbase + rj) * ST;
+      const float* xr = lds + (gbase + rid) * ST;
       float n4[4] = {0.0f, 0.0f, 0.0f, 0.0f}, d4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int k = 0; k < D; k += 4) {
         const float4 v = *reinterpret_cast<const float4*>(cr + k);
+        const float4 u = *reinterpret_cast<const float4*>(xr + k);
         n4[0] = n4[0] + v.x * v.x;
         n4[1] = n4[1] + v.y * v.y;
         n4[2] = n4[2] + v.z * v.z;
         n4[3] = n4[3] + v.w * v.w;
-        d4[0] = d4[0] + x[k] * v.x;
-        d4[1] = d4[1] + x[k + 1] * v.y;
-        d4[2] = d4[2] + x[k + 2] * v.z;
-        d4[3] = d4[3] + x[k + 3] * v.w;
+        d4[0] = d4[0] + u.x * v.x;
+        d4[1] = d4[1] + u.y * v.y;
+        d4[2] = d4[2] + u.z * v.z;
+        d4[3] = d4[3] + u.w * v.w;
       }
       uint32_t dn = 0u;
       if (need) {
@@ -361,14 +366,15 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
 #pragma unroll
         for (int k = 0; k < D; k += 4) {
           const float4 v = *reinterpret_cast<const float4*>(cr + k);
+          const float4 u = *reinterpret_cast<const float4*>(xr + k);
           nn = nn + v.x * v.x;
           nn = nn + v.y * v.y;
           nn = nn + v.z * v.z;
           nn = nn + v.w * v.w;
-          dot = dot + x[k] * v.x;
-          dot = dot + x[k + 1] * v.y;
-          dot = dot + x[k + 2] * v.z;
-          dot = dot + x[k + 3] * v.w;
+          dot = dot + u.x * v.x;
+          dot = dot + u.y * v.y;
+          dot = dot + u.z * v.z;
+          dot = dot + u.w * v.w;
         }
         if (dn == 2u) dn = decide(dc, dot, sq * __builtin_sqrtf(nn)) ? 1u : 0u;
       }
@@ -1398,23 +1404,42 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
     for (uint32_t a = t; a < b; a += NT) {
       const uint32_t s = slots[p + a];
       slot[a] = s;
-      nrm[a] = r.nrm[s];
-      sq[a] = __builtin_sqrtf(nrm[a]);
+      if constexpr (!ROWS_LDS) {
+        nrm[a] = r.nrm[s];
+        sq[a] = __builtin_sqrtf(nrm[a]);
+      }
       cnt[a] = r.cnt[s];
       hd[a] = r.head[s];
       tl[a] = r.tail[s];
       pos2row[a] = a;
     }
     for (uint32_t a = t; a < b * (uint32_t)W; a += NT) P[a] = 0ull;
-    __syncthreads();
     if constexpr (ROWS_LDS) {
+      // the rows in the same round of loads as the metadata (each lane reads its row's slot
+      // itself: no barrier, and so no second memory latency, between the two)
       for (uint32_t q = t; q < b * (uint32_t)(D / 4); q += NT) {
         const uint32_t a = q / (D / 4), k = (q % (D / 4)) * 4;
         *reinterpret_cast<float4*>(rows + a * ST + k) =
-            *reinterpret_cast<const float4*>(r.x + (size_t)slot[a] * r.dp + k);
+            *reinterpret_cast<const float4*>(r.x + (size_t)slots[p + a] * r.dp + k);
       }
       __syncthreads();
+      // norms recomputed from the rows in LDS (the cached chain, distance.cc:33-34: same bits)
+      // instead of a random 4-B read each
+      for (uint32_t a = t; a < b; a += NT) {
+        float n = 0.0f;
+#pragma unroll
+        for (int k = 0; k < D; k += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(rows + a * ST + k);
+          n = n + v.x * v.x;
+          n = n + v.y * v.y;
+          n = n + v.z * v.z;
+          n = n + v.w * v.w;
+        }
+        nrm[a] = n;
+        sq[a] = __builtin_sqrtf(n);
+      }
     }
+    __syncthreads();
 
     // decisions in 64x64 tiles (row block R, column block C <= R): lanes = rows of R with the
     // row in registers, columns walked in order (LDS broadcast); the wave's ballot at column c
@@ -1863,9 +1888,6 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
   const int d = r.d, dp = r.dp;
   const bool valid = g < b;
   float nrm = valid ? r.nrm[slot] : 0.0f;
-  uint32_t cnt = valid ? r.cnt[slot] : 0u;
-  uint32_t hd = valid ? r.head[slot] : 0u;
-  const uint32_t tl = valid ? r.tail[slot] : 0u;
   float sq = __builtin_sqrtf(nrm);  // distance.cc:37
   const float* myx = r.x + (size_t)slot * dp;
   const uint32_t bmax = wave_max(b);
@@ -1913,6 +1935,15 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
         full |= (uint64_t)in << src;
       }
     }
+  }
+
+  // member counts and list ends only for the runs with a matching pair (as merge_batch)
+  const bool grp = (__ballot(valid && full != 0ull) & gmask) != 0ull;
+  uint32_t cnt = 0u, hd = 0u, tl = 0u;
+  if (valid && grp) {
+    cnt = r.cnt[slot];
+    hd = r.head[slot];
+    tl = r.tail[slot];
   }
 
   // 2. the walk, replayed on the bits (as merge_batch); rows live in memory
@@ -1971,7 +2002,7 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
 
   // 3. write back
   const uint32_t pos_slot = shfl32(slot, gbase + rowid);
-  if (valid) slots[p + g] = g < size ? pos_slot : kInvalid;
+  if (valid && size < b) slots[p + g] = g < size ? pos_slot : kInvalid;
   if (valid && alive && dirty) {
     r.nrm[slot] = nrm;
     r.cnt[slot] = cnt;
