@@ -2276,7 +2276,12 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   // every small-run class in one persistent launch (the kernel strides over its batches)
   if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
-  k_merge_small<D><<<4608, 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
+  // 12288 one-wave workgroups, 6 per resident slot (2048 at 2 waves per SIMD): the batch stride
+  // of a persistent wave is long enough that its rows come from all over the lists, and waves
+  // retire and re-enter as the big-run workgroups come and go (C2, same box, interleaved:
+  // 4608 -> 255.9 / 258.0 ms, 8192 -> 255.4 / 252.3, 12288 -> 250.8 / 251.7, 16384 -> 256.0 /
+  // 253.9; small-run merge 79.4 -> 70.5 ms per step)
+  k_merge_small<D><<<12288, 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
   if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[1], f.lane(2));
 }
 
