@@ -191,12 +191,53 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
         cost.append(secs / max(1, n_t))
     per_row = np.interp(np.arange(len(trace)), ts, cost)
     t_loop = float((trace * per_row).sum())
+    c1 = c1_measured(harness, threads) if kind == "reference" else None
     return {"value": n0 * iters / t_loop, "unit": "k-mers·iterations/s", "cores": threads,
+            "c1_measured": c1,
             "kind": kind, "estimated_loop_s": round(t_loop, 2), "sample_seconds": round(secs_all, 2),
             "sample": (f"one iteration of the main loop from its own state at t = "
                        f"{', '.join(map(str, ts))} of {iters} ({threads} threads, threshold 0.95); "
                        f"per-row cost interpolated in t and weighted by the loop's N_t trace "
                        f"(sum N_t = {int(trace.sum())}) to estimate T_loop")}
+
+
+def c1_measured(harness, threads):
+    """The reference's WHOLE main loop on C1 (BASELINE configs[0]: 100K x 8, -I 10 -N 0.80), timed:
+    the C1 workload through the engine's convert + init pass (GPU), then the reference's own
+    Cluster() (ref_harness) over all 10 iterations from that state, and the engine's loop on the
+    same state for comparison.  A measured full loop beside C2's sampled estimate."""
+    from kmerlsh_amd import _native
+
+    n0, d, iters, min_sim, seed, _ = CONFIGS["c1"]
+    eng = _native.Engine(0)
+    try:
+        counter0, kept, _ = prepare(eng, n0, d, seed)
+        rows, off, ids = eng.result()
+        n_t = rows.shape[0]
+        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
+            src = os.path.join(tmp, "rows.f32")
+            rows.astype("<f4").tofile(src)
+            off.astype("<u8").tofile(src + ".off")
+            ids.astype("<u8").tofile(src + ".ids")
+            env = dict(os.environ, OMP_THREAD_LIMIT=str(threads), OMP_NUM_THREADS=str(threads),
+                       KLSH_REF_THREADS=str(threads), KLSH_SEED=str(SEED_BASE))
+            out = subprocess.run([harness, "cluster_w", src, src + ".off", src + ".ids", str(n_t),
+                                  str(d), repr(float(min_sim)), str(iters), "1000000",
+                                  os.path.join(tmp, "out")], env=env, check=True,
+                                 capture_output=True, text=True, timeout=600).stdout
+        secs = float(re.findall(r"hash\+cluster takes \(secs\): ([0-9.eE+-]+)", out)[-1])
+        eng.restore()
+        t0 = time.perf_counter()
+        eng.cluster(min_sim, iters, 1_000_000, SEED_BASE, counter0)
+        gpu = time.perf_counter() - t0
+    finally:
+        eng.close()
+    log(f"C1 full loop: reference {secs:.3f} s ({threads} threads), engine {gpu * 1e3:.2f} ms")
+    return {"loop_s": secs, "value": n0 * iters / secs, "unit": "k-mers·iterations/s",
+            "cores": threads, "rows_after_init": int(n_t),
+            "engine_loop_ms": round(gpu * 1e3, 3), "engine_value": n0 * iters / gpu,
+            "note": "C1 (100K x 8, -I 10): the reference's whole main loop timed (ref_harness), "
+                    "from the engine's post-init state; engine timed on the same state"}
 
 
 def check_parity(config, trace, counter, result):
@@ -231,6 +272,118 @@ def pmc_traffic(config, kernel):
     with open(path) as f:
         data = json.load(f)
     return (data.get(config) or {}).get(kernel)
+
+
+# Algorithmic bytes of one kernel class over a step, from the class's own row
+# counters (klsh_stats.kern: rows handled, runs) — what the class must move at minimum:
+#   project   rows x (4d row + 4 slot + 4 key)
+#   sort      sum over iterations of N_t x passes_t x 20 (hist: key; scatter: key + slot in and out)
+#   runs      rows x 4 (sorted keys) + runs x 8 (list entries)
+#   small     rows x (4d + 4) (row + slot) + merges x (4d + 20) (new row, norm, count, head, link)
+#   big*/huge rows x (4d + 20) (row, slot, count, head, tail, the slot written back)
+#   tail      rows x (4d + 8) (all merge classes of a small iteration in one launch)
+#   compact   rows x 12 (slots read twice, survivors written)
+KERNEL_NAMES = {
+    "project": "k_project_pk<{d}>", "sort": "k_sort_hist/dscan/scatter (span)",
+    "runs": "k_runs_count/scan/write (span)", "small": "k_merge_small<{d}>",
+    "big128": "k_merge_big<{d},128,128,true>", "big192": "k_merge_big<{d},192,256,true>",
+    "big384": "k_merge_big<{d},384,256,true>", "big896": "k_merge_big<{d},896,256,false>",
+    "huge": "k_merge_huge<{d}>", "tail": "k_merge_tail<{d}>",
+    "compact": "k_compact_count/apply (span)",
+}
+WIDE_NAMES = {
+    "project": "k_project_mfma_wide + k_project_fix (span)",
+    "small": "k_merge_group_wide<64..2> (chain on one stream, span)",
+    "big128": "k_merge_big_wide<128,128,32>", "big192": "k_merge_big_wide<384,256,32>",
+    "big384": "k_merge_big_wide<384,256,32>", "big896": "k_merge_big_wide<896,256,16>",
+    "huge": "k_merge_huge<0>",
+}
+BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def kernel_rooflines(config, stats, steps, d, trace):
+    """Every kernel class's achieved HBM rate (its algorithmic bytes per launch over its average
+    HIP-event launch time); the headline is the class with the largest time per step."""
+    import math
+
+    register = d in (8, 16, 32, 64)
+    kern = {c: {f: sum(s["kern"][c][f] for s in stats) for f in ("ms", "launches", "rows", "runs")}
+            for c in stats[0]["kern"]}
+    merges_small = sum(s["small_iter_merges"] for s in stats)
+    tr = np.asarray(trace, dtype=np.float64)
+    tr = tr[tr > 1]
+    passes = np.ceil(np.floor(np.log2(tr)) / 10.0) if tr.size else tr
+    sort_bytes = float((tr * passes * 20.0).sum()) * steps
+    out = []
+    for c, k in kern.items():
+        if not k["launches"] or k["ms"] <= 0:
+            continue
+        rows, runs = k["rows"], k["runs"]
+        b = {"project": rows * (4 * d + 8), "sort": sort_bytes, "runs": rows * 4 + runs * 8,
+             "small": rows * (4 * d + 4) + merges_small * (4 * d + 20),
+             "tail": rows * (4 * d + 8), "compact": rows * 12}.get(c, rows * (4 * d + 20))
+        avg = k["ms"] / k["launches"]
+        ach = (b / k["launches"]) / (avg * 1e-3) / 1e9
+        name = (KERNEL_NAMES if register or c not in WIDE_NAMES else WIDE_NAMES)[c].format(d=d)
+        pmc = pmc_traffic(config, c) or pmc_traffic(config, {"project": "k_project",
+                                                             "small": "k_merge_small"}.get(c, ""))
+        e = {"kernel": name, "class": c, "bound": "hbm", "achieved": round(ach, 2),
+             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+             "traffic_source": (pmc or {}).get("source"),
+             "bytes_per_launch": b / k["launches"], "avg_launch_ms": avg,
+             "launches_per_step": k["launches"] / steps, "ms_per_step": k["ms"] / steps,
+             "rows_per_launch": rows / k["launches"]}
+        # the same launches through HIP events on their own stream, where that measures the
+        # kernel (the projection and the small-run launch run alone on theirs; a big-run class
+        # shares the CUs with them and an event pair would include its waits for resources)
+        ev_ms = {"project": sum(s["project_ms"] for s in stats),
+                 "small": sum(s["small_ms"] for s in stats)}.get(c)
+        ev_n = {"project": sum(s["project_launches"] for s in stats),
+                "small": sum(s["small_launches"] for s in stats)}.get(c)
+        e["timing"] = "stamps"
+        if ev_ms and ev_n:
+            e["hip_events"] = {"avg_launch_ms": ev_ms / ev_n, "launches_per_step": ev_n / steps,
+                               "ms_per_step": ev_ms / steps}
+            if ev_n == k["launches"]:
+                # the HIP-event time of the same launches is the reported rate; stamps beside it
+                ev_avg = ev_ms / ev_n
+                ach_ev = (b / k["launches"]) / (ev_avg * 1e-3) / 1e9
+                e["stamps"] = {"achieved": e["achieved"], "frac": e["frac"], "avg_launch_ms": avg}
+                e["stamps"]["ms_per_step"] = e["ms_per_step"]
+                e.update(achieved=round(ach_ev, 2), frac=round(ach_ev / HBM_PEAK_GBS, 5),
+                         avg_launch_ms=ev_avg, ms_per_step=ev_ms / steps, timing="hip_events")
+        if c == "project":
+            bits = sum(s["sum_proj_bits"] for s in stats)
+            if register:
+                # one v_pk_mul + one v_pk_add per two row-hyperplane MACs (bit-exactness forbids
+                # fusing): 256 CU x 4 SIMD x 32 lanes x 2 flop x 2.4 GHz / 2 = 78.6 Tflop/s
+                fl = 2.0 * bits * d / k["launches"]
+                e["valu"] = {"achieved": round(fl / (avg * 1e-3) / 1e12, 2), "peak": VALU_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "note": "separate f32 mul + add (no FMA: bit-exact "
+                                                        "with the reference), packed v_pk_mul/v_pk_add"}
+                e["valu"]["frac"] = round(e["valu"]["achieved"] / VALU_PEAK_TFLOPS, 4)
+            else:
+                # the certified screen: S = X W^T as bf16x3 (hi.hi + hi.lo + lo.hi), 3 bf16 MFMA
+                # products per f32 product, against the dense bf16 peak; the exact fix-up of the
+                # close calls is in the span too
+                fl = 3 * 2.0 * bits * d / k["launches"]
+                e["mfma"] = {"achieved": round(fl / (avg * 1e-3) / 1e12, 2),
+                             "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                             "note": "bf16x3 split on v_mfma_f32_32x32x16_bf16 (3 products per f32 "
+                                     "product); span includes k_project_fix"}
+                e["mfma"]["frac"] = round(e["mfma"]["achieved"] / BF16_DENSE_TFLOPS, 5)
+        out.append(e)
+    if not out:
+        return {}
+    head = dict(max(out, key=lambda e: e["ms_per_step"]))
+    head["kernels"] = sorted(out, key=lambda e: -e["ms_per_step"])
+    head["note"] = ("roofline = the kernel class with the largest time per step; a launch's time "
+                    "is its first workgroup start -> last workgroup end from in-kernel "
+                    "s_memrealtime stamps (rocprofv3's kernel span), hip_events = the HIP event "
+                    "pair on the launch's own stream where that isolates it; 'span' classes cover "
+                    "several dependent launches")
+    return head
 
 
 def main():
@@ -291,56 +444,18 @@ def main():
     if parity.get("checked"):
         log(f"parity vs {parity['fixture']}: {'ok' if parity['ok'] else 'MISMATCH'}")
     value = (1 if sharded else world) * n0 * iters * args.steps / elapsed
-    agg = {k: sum(s[k] for s in stats) for k in stats[0]}
+    agg = {k: sum(s[k] for s in stats) for k in stats[0] if k != "kern"}
     phases = {p: agg[p + "_ms"] / args.steps
               for p in ("project", "sort", "merge", "compact", "host", "comm", "small")}
+    for c in ("runs", "tail", "compact"):
+        phases[c] = sum(s["kern"][c]["ms"] for s in stats) / args.steps
     # Kernel rooflines.  The projection: algorithmic bytes per launch = rows x
     # (4d row + 4 slot + 4 key).  The small-run merge (runs of 2..64 rows; its own launch in the
     # iterations of >= 2^20 positions, ~83 ms of a C2 step, timed by HIP events on its stream):
     # rows x (4d row + 4 slot) + merges x (4d new row + 20 metadata: norm, count, head, member
     # link, the removed row's count) — merges counted over the whole iteration (~97 % of them are
     # small-run merges on C2).  The bench line's "roofline" is the one with the larger time per step.
-    launches = agg["project_launches"]
-    proj_bytes = agg["sum_rows"] * (4 * d + 8)      # row read + slot read + key write
-    avg_ms = agg["project_ms"] / max(1, launches)
-    achieved = (proj_bytes / max(1, launches)) / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    # the same launches against the packed-f32 VALU ceiling: one v_pk_mul + one v_pk_add per two
-    # row-hyperplane MACs (bit-exactness forbids fusing), 256 CU x 4 SIMD x 16 lanes x 2 x 2 flop
-    # x 2.4 GHz = 78.6 Tflop/s (half the FMA-counted 157.3 TF vector peak)
-    valu_flops = 2.0 * agg["sum_proj_bits"] * d / max(1, launches)
-    valu_achieved = valu_flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    pname = f"k_project_pk<{d}>" if d in (8, 16, 32, 64) else "k_project_mfma_wide"
-    ptraffic = pmc_traffic(args.config, "k_project")
-    project = {
-        "kernel": pname, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-        "traffic": ptraffic.get("hbm_bytes_per_launch") if ptraffic else None,
-        "traffic_source": (ptraffic or {}).get("source"),
-        "bytes_per_launch": proj_bytes / max(1, launches), "avg_launch_ms": avg_ms,
-        "launches_per_step": launches / args.steps, "ms_per_step": agg["project_ms"] / args.steps,
-        "valu": {"achieved": round(valu_achieved, 2), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                 "frac": round(valu_achieved / VALU_PEAK_TFLOPS, 4),
-                 "note": "separate f32 mul+add (no FMA: bit-exact with the reference), packed"},
-    }
-    kernels = [project]
-    if agg.get("small_launches"):
-        sl = agg["small_launches"]
-        s_bytes = agg["small_rows"] * (4 * d + 4) + agg["small_iter_merges"] * (4 * d + 20)
-        s_ms = agg["small_ms"] / sl
-        s_ach = (s_bytes / sl) / (s_ms * 1e-3) / 1e9 if s_ms > 0 else 0.0
-        straffic = pmc_traffic(args.config, "k_merge_small")
-        kernels.append({
-            "kernel": f"k_merge_small<{d}>", "bound": "hbm", "achieved": round(s_ach, 2),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(s_ach / HBM_PEAK_GBS, 5),
-            "traffic": straffic.get("hbm_bytes_per_launch") if straffic else None,
-            "traffic_source": (straffic or {}).get("source"),
-            "bytes_per_launch": s_bytes / sl, "avg_launch_ms": s_ms,
-            "launches_per_step": sl / args.steps, "ms_per_step": agg["small_ms"] / args.steps,
-            "rows_per_launch": agg["small_rows"] / sl,
-            "note": "the iterations of >= 2^20 positions (below that the small runs merge inside "
-                    "k_merge_tail with the big runs)"})
-    roofline = dict(max(kernels, key=lambda k: k["ms_per_step"]))
-    roofline["kernels"] = kernels
+    roofline = kernel_rooflines(args.config, stats, args.steps, d, trace)
     # the whole loop against HBM, SURVEY.md §8(d): B_t = N_t (8d + 16) + M_t (4d + 8) bytes per
     # iteration (rows read by the projection and by the merge, keys and order written and read;
     # per merge the new row and a member link), summed over the timed steps

@@ -39,6 +39,28 @@ extern "C" {
 
 typedef struct klsh_ctx klsh_ctx;
 
+/* Per-kernel-class statistics of a call: HIP-event time of the class's launches (events bound to
+ * the dispatches themselves), launches, and the rows they handled (the unit of each class's
+ * algorithmic bytes).  Index = KLSH_K_*. */
+#define KLSH_K_PROJECT 0  /* sign-hash of every live row (k_project_*) */
+#define KLSH_K_SORT 1     /* stable bucket sort, all passes (span of the first to last launch) */
+#define KLSH_K_RUNS 2     /* run finding and size-class lists (span) */
+#define KLSH_K_SMALL 3    /* runs of 2..64 rows (k_merge_small; d > 64: the k_merge_group_wide chain) */
+#define KLSH_K_BIG128 4   /* runs of 65..128 rows (k_merge_big / k_merge_big_wide) */
+#define KLSH_K_BIG192 5   /* 129..192 */
+#define KLSH_K_BIG384 6   /* 193..384 */
+#define KLSH_K_BIG896 7   /* 385..896 */
+#define KLSH_K_HUGE 8     /* longer runs (k_merge_huge) */
+#define KLSH_K_TAIL 9     /* iterations below 2^20 positions: every merge class in one k_merge_tail */
+#define KLSH_K_COMPACT 10 /* survivor compaction (span) */
+#define KLSH_KCLASSES 12
+typedef struct klsh_kstat {
+  double ms;
+  uint64_t launches;
+  uint64_t rows;
+  uint64_t runs;
+} klsh_kstat;
+
 /* Per-call statistics (all times are milliseconds). */
 typedef struct klsh_stats {
   uint64_t iterations;     /* iterations run */
@@ -64,6 +86,8 @@ typedef struct klsh_stats {
   uint64_t small_launches;
   uint64_t small_rows;
   uint64_t small_iter_merges;
+  /* per kernel class (single-GPU loop; option "kernel_timing", default on) */
+  klsh_kstat kern[KLSH_KCLASSES];
 } klsh_stats;
 
 /* ---- lifetime ------------------------------------------------------------------------------- */
@@ -115,8 +139,8 @@ int klsh_comm_init_local(klsh_ctx** ctxs, int world);
 int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
 /* Options: "shard_min_rows" (sharded loop: below this many live rows every rank runs the
  * remaining iterations on its own replica, without exchanges; default 2097152 = 2^21, 0 = always
- * sharded), "phase_timing" (0/1: per-phase HIP events, adds latency) — results never depend on
- * either; "stop_after" (k > 0: klsh_cluster runs only the first k iterations of its threshold
+ * sharded), "phase_timing" (0/1: per-phase HIP events, adds latency), "kernel_timing" (0/1,
+ * default 1: the per-class statistics of klsh_stats.kern) — results never depend on them; "stop_after" (k > 0: klsh_cluster runs only the first k iterations of its threshold
  * schedule, e.g. to pin a prefix of a long loop; 0 = all, the default), "hyperplane_window"
  * (hyperplane rows drawn up front per call; the rest are drawn when the loop reaches them; 0 =
  * the default: all of them while they fit in 256 MB, else 64 iterations' worth). */
@@ -205,14 +229,25 @@ int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* set, const char* in_path,
  * as kmer/kmc_api/kmc_file.cpp:66-532): the union of canonical k-mers over the samples, each
  * sample's summed counts clamped at 65535, written to <out_dir>/ kmer_set.hex (8 bytes per k-mer),
  * kmer_count.bin (sample-major uint16) and kmer_count.log ("%llu" rows, "\t%f" coverage = float sum
- * of log(count) per sample).  The rows, counts and log equal the reference's; the reference's row
- * ORDER is its hash table's (libcuckoo), here it is first appearance (sample, then file order).
+ * of log(count) per sample).  The files equal the reference's byte for byte: rows in the order of its
+ * libcuckoo table after KmcRead's inserts at -T 1 (while the table never grows; a growing
+ * reference table re-inserts from hardware_concurrency() threads, and that order is replayed here
+ * as if those threads ran one after another).
  * out_dir NULL or "" = the current directory.  stats may be NULL. */
 typedef struct klsh_khtable_stats {
   uint64_t kmap_size, records, records_listed;
   double io_ms;     /* host reads of the .kmc_suf streams */
   double total_ms;
+  double order_ms;  /* host replay of the reference's libcuckoo inserts (the row order) */
 } klsh_khtable_stats;
+/* The row order alone (a test hook): the libcuckoo table order (kmer/Kmer.cc:138 hash, the
+ * vendored utils/libcuckoo/cuckoohash_map.hh, 8-slot buckets, 2^16 buckets to start) of n DISTINCT
+ * k-mer images inserted in the given order: order[i] = index of the table's i-th element.  Returns
+ * the table's final hash power (>= 16), or a negative KLSH_E_* code.  Host only. */
+int klsh_cuckoo_order(const uint64_t* images, uint64_t n, int k, uint32_t* order);
+/* The host parse of a KMC database's prefix file (<name>.kmc_pre: version, header, prefix LUT) as
+ * klsh_build_khtable does it, every file-derived offset checked (a test hook).  Host only. */
+int klsh_kmc_info(const char* name, int* k, uint64_t* total, uint64_t* lut_entries);
 int klsh_build_khtable(klsh_ctx* ctx, const char* const* kmc_names, int n_samples, int k,
                        const char* out_dir, klsh_khtable_stats* stats);
 

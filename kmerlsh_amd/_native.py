@@ -34,8 +34,24 @@ EXPORTED = (
     "klsh_synth_counts", "klsh_comm_unique_id", "klsh_comm_init", "klsh_comm_init_local",
     "klsh_comm_info", "klsh_set_option", "klsh_wrs", "klsh_ttest2", "klsh_fastq_open",
     "klsh_fastq_next", "klsh_fastq_close", "klsh_kset_create", "klsh_kset_destroy",
-    "klsh_check_reads", "klsh_extract_fastq", "klsh_build_khtable",
+    "klsh_check_reads", "klsh_extract_fastq", "klsh_build_khtable", "klsh_cuckoo_order",
+    "klsh_kmc_info",
 )
+
+
+# klsh_stats.kern indices (include/klsh.h KLSH_K_*)
+KERNEL_CLASSES = ("project", "sort", "runs", "small", "big128", "big192", "big384", "big896",
+                  "huge", "tail", "compact")
+KCLASSES = 12
+
+
+class KlshKstat(ctypes.Structure):
+    _fields_ = [
+        ("ms", ctypes.c_double),
+        ("launches", ctypes.c_uint64),
+        ("rows", ctypes.c_uint64),
+        ("runs", ctypes.c_uint64),
+    ]
 
 
 class KlshStats(ctypes.Structure):
@@ -60,10 +76,14 @@ class KlshStats(ctypes.Structure):
         ("small_launches", ctypes.c_uint64),
         ("small_rows", ctypes.c_uint64),
         ("small_iter_merges", ctypes.c_uint64),
+        ("kern", KlshKstat * KCLASSES),
     ]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "kern"}
+        d["kern"] = {name: {f: getattr(self.kern[i], f) for f, _ in KlshKstat._fields_}
+                     for i, name in enumerate(KERNEL_CLASSES)}
+        return d
 
 
 class KlshExtractStats(ctypes.Structure):
@@ -90,6 +110,7 @@ class KlshKhtableStats(ctypes.Structure):
         ("records_listed", ctypes.c_uint64),
         ("io_ms", ctypes.c_double),
         ("total_ms", ctypes.c_double),
+        ("order_ms", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -160,8 +181,12 @@ def load_library() -> ctypes.CDLL:
                                               ctypes.c_int, ctypes.c_float, _P]),
         "klsh_build_khtable": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
                                               ctypes.c_int, ctypes.c_char_p, _P]),
+        "klsh_cuckoo_order": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, _P]),
+        "klsh_kmc_info": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), _u64p, _u64p]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("KLSH_LIB") and not hasattr(lib, name):
+            continue  # an A/B build of an older engine: entry points it predates stay unbound
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -201,6 +226,18 @@ def comm_init_local(engines) -> None:
     lib = load_library()
     arr = (ctypes.c_void_p * len(engines))(*[e._ctx for e in engines])
     _check(lib.klsh_comm_init_local(arr, len(engines)), "klsh_comm_init_local")
+
+
+def cuckoo_order(images: np.ndarray, k: int) -> tuple[np.ndarray, int]:
+    """The reference's libcuckoo table order of distinct k-mer images inserted in the given order
+    (host): (index of each table element in iteration order, final hash power)."""
+    lib = load_library()
+    im = np.ascontiguousarray(images, np.uint64)
+    out = np.zeros(im.size, np.uint32)
+    hp = lib.klsh_cuckoo_order(_ptr(im), im.size, k, _ptr(out))
+    if hp < 0:
+        _check(hp, "klsh_cuckoo_order")
+    return out, int(hp)
 
 
 def synth_counts(n: int, d: int, seed: int, genomes: int = 0, threads: int = 0):

@@ -404,7 +404,11 @@ int main(int argc, char** argv) {
     return 2;
   }
   uint64_t counter = 0;
-  const uint64_t batch_thresh = 100000000ull;
+  // app/kmerLSH.cc's 1e8-row batch size; KLSH_TEST_BATCH_THRESH overrides it for the tests that
+  // pin the multi-batch init and re-cluster branch against the oracle's CLI (never set otherwise)
+  uint64_t batch_thresh = 100000000ull;
+  if (const char* e = getenv("KLSH_TEST_BATCH_THRESH"))
+    if (strtoull(e, nullptr, 10) >= 1000) batch_thresh = strtoull(e, nullptr, 10);
   float similarity = min_sim;
   RowSet cur;
   cur.d = d;

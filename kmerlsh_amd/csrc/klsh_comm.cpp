@@ -6,7 +6,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -29,6 +31,36 @@ struct RcclComm final : Comm {
     aborted = true;
     if (nc) (void)ncclCommAbort(nc);
     nc = nullptr;
+  }
+  int wait(hipStream_t s) override {
+    if (aborted) return check(ncclSuccess, "wait");
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t polls = 0;; ++polls) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) return 0;
+      if (q != hipErrorNotReady) {
+        err = std::string("stream: ") + hipGetErrorString(q);
+        abort();
+        return -1;
+      }
+      if ((polls & 255u) == 0) {
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(nc, &ae) != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress)) {
+          err = std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae);
+          abort();
+          return -1;
+        }
+        const double secs =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (secs > timeout_s) {
+          err = "collective timed out after " + std::to_string((int)secs) +
+                " s (a peer rank failed or stopped); communicator aborted";
+          abort();
+          return -1;
+        }
+      }
+      __builtin_ia32_pause();
+    }
   }
   int check(ncclResult_t r, const char* what) {
     if (aborted) {
@@ -113,6 +145,10 @@ Comm* make_rccl_comm(int rank, int world, const void* unique_id, int device, std
   auto c = std::make_unique<RcclComm>();
   c->rank = rank;
   c->world = world;
+  if (const char* e = getenv("KLSH_COMM_TIMEOUT_S")) {
+    const double v = atof(e);
+    if (v > 0.0) c->timeout_s = v;
+  }
   const ncclResult_t r = ncclCommInitRank(&c->nc, world, id, rank);
   if (r != ncclSuccess) {
     if (err) *err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);

@@ -44,6 +44,20 @@ struct Comm {
   // of waiting forever for this rank (RCCL: ncclCommAbort; in-process group: wake every waiter).
   // The communicator is unusable afterwards.
   virtual void abort() = 0;
+  // Wait for stream s, which may hold this group's collectives.  RCCL: polls the stream together
+  // with ncclCommGetAsyncError, and after an asynchronous error — or no progress for
+  // timeout_s seconds (a peer that failed and will never post its half) — aborts the
+  // communicator and returns -1, so a rank never blocks forever in a collective its peers
+  // abandoned.  The in-process group: a plain stream sync (its collectives are host barriers that
+  // an abort already wakes).
+  virtual int wait(hipStream_t s) {
+    if (hipStreamSynchronize(s) != hipSuccess) {
+      err = "stream sync";
+      return -1;
+    }
+    return 0;
+  }
+  double timeout_s = 600.0;  // KLSH_COMM_TIMEOUT_S
   bool aborted = false;
   std::string err;
 };

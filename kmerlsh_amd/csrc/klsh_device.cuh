@@ -6,6 +6,41 @@
 #include "klsh_internal.h"
 
 namespace klsh {
+// ---- per-kernel-class stamps (KStampBlock, klsh_internal.h) ----------------------------------
+__device__ __forceinline__ unsigned long long stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
+// the workgroup's start / end (thread 0; its waves end within a few microseconds of each other)
+__device__ __forceinline__ void kt_begin(const KTime& kt, int c) {
+  if (kt.blk && threadIdx.x == 0)
+    atomicMin(&kt.blk->set[kt.set].t0[c][blockIdx.x % kStampSlots].v, stamp_now());
+}
+__device__ __forceinline__ void kt_end(const KTime& kt, int c) {
+  if (kt.blk && threadIdx.x == 0)
+    atomicMax(&kt.blk->set[kt.set].t1[c][blockIdx.x % kStampSlots].v, stamp_now());
+}
+// set `f`'s spans into the totals, then cleared; threads [0, KC_COUNT) of one workgroup
+__device__ __forceinline__ void kt_fold_set(KStampBlock* blk, int f, uint32_t t) {
+  if (t >= (uint32_t)KC_COUNT) return;
+  KStampSet& st = blk->set[f];
+  unsigned long long lo = ~0ull, hi = 0ull;
+  for (int q = 0; q < kStampSlots; ++q) {
+    lo = min(lo, __hip_atomic_load(&st.t0[t][q].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    hi = max(hi, __hip_atomic_load(&st.t1[t][q].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __hip_atomic_store(&st.t0[t][q].v, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st.t1[t][q].v, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (hi != 0ull && lo != ~0ull && hi >= lo) {
+    blk->ticks[t] += hi - lo;
+    blk->launches[t] += 1ull;
+  }
+}
+// the projection's first workgroup folds the previous iteration's set
+__device__ __forceinline__ void kt_fold(const KTime& kt) {
+  if (kt.blk && kt.fold >= 0 && blockIdx.x == 0) kt_fold_set(kt.blk, kt.fold, threadIdx.x);
+}
+}  // namespace klsh
+
+
+namespace klsh {
 
 // ============================================================================ helpers ==========
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }

@@ -96,7 +96,16 @@ struct klsh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[8] = {};
-  hipEvent_t sev[2] = {};  // around the small-run merge launch (bench roofline)
+  hipEvent_t sev[2] = {};  // around the small-run merge launch (HIP-event cross-check)
+  // per-kernel-class stamps (klsh_stats.kern, KStampBlock in klsh_internal.h): the timed
+  // iterations of a call stamp sets kt_iter & 1 in turn
+  klsh::KStampBlock* kstamp = nullptr;
+  uint64_t kt_iter = 0;
+  klsh::LookBack lb{nullptr, 0};  // the one-launch compaction of small iterations
+  bool kernel_timing = [] {
+    const char* e = getenv("KLSH_KERNEL_TIMING");
+    return !(e && e[0] == '0');
+  }();
 
   // sizes
   int d = 0, dp = 0;
@@ -246,6 +255,8 @@ struct klsh_ctx {
     pw.cap = 0;
     for (auto& c : mw.big) dfree(c);
     for (auto& c : mw.cls) dfree(c);
+    dfree(kstamp);
+    dfree(lb.status);
     cap_slots = cap_members = 0;
     cap_dp = 0;
     drop_snapshot();
@@ -331,6 +342,27 @@ struct klsh_ctx {
         hipMemset(tile_sums, 0, sizeof(uint32_t) * klsh::scan_ws_words(s)) != hipSuccess) {
       release_state();
       return fail(KLSH_E_HIP, "workspace init");
+    }
+    // The stamp block and the look-back status words: small buffers allocated AFTER the rows and
+    // workspaces.  (Allocated at context creation, ahead of the multi-GB state, they cost a C2 step
+    // 252 -> 330 ms on MI355X: every random-access kernel slowed, the sort scatter 2.5x — the
+    // large buffers evidently lost their large-page backing; A/B in DESIGN.md §6.)
+    {
+      std::vector<unsigned char> init(sizeof(klsh::KStampBlock), 0);
+      auto* b = reinterpret_cast<klsh::KStampBlock*>(init.data());
+      for (auto& st : b->set)
+        for (auto& cls : st.t0)
+          for (auto& ln : cls) ln.v = ~0ull;  // every start line ~0, every end line and total 0
+      if ((e = dalloc(&kstamp, 1)) || (e = dalloc(&lb.status, 256))) {
+        release_state();
+        return e;
+      }
+      if (hipMemcpy(kstamp, init.data(), init.size(), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemset(lb.status, 0, sizeof(unsigned long long) * 256) != hipSuccess) {
+        release_state();
+        return fail(KLSH_E_HIP, "stamp / look-back init");
+      }
+      lb.epoch = 0;
     }
     mw.tile_sums = tile_sums;
     cap_slots = s;
@@ -440,6 +472,50 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 
 }  // namespace
 
+// Rows per kernel class of one iteration (the unit of each class's algorithmic bytes), from the
+// counters that iteration published.  tail: the iteration ran every merge class in k_merge_tail.
+static void count_class_rows(klsh_stats* st, const Counters& c, uint64_t n, bool tail) {
+  using namespace klsh;
+  uint64_t big_rows = 0, big_runs = 0, small_runs = 0;
+  for (int b = 0; b < kBigClasses; ++b) big_rows += c.n_big_rows[b], big_runs += c.n_big[b];
+  for (int b = 0; b < kGroupClasses; ++b) small_runs += c.n_cls[b];
+  for (int k : {KC_PROJECT, KC_SORT, KC_COMPACT}) st->kern[k].rows += n;
+  st->kern[KC_RUNS].rows += n;
+  st->kern[KC_RUNS].runs += c.n_seg;
+  st->kern[KC_HUGE].rows += c.n_huge_rows;
+  st->kern[KC_HUGE].runs += c.n_huge;
+  if (tail) {
+    st->kern[KC_TAIL].rows += c.n_small_rows + big_rows;
+    st->kern[KC_TAIL].runs += small_runs + big_runs;
+    return;
+  }
+  st->kern[KC_SMALL].rows += c.n_small_rows;
+  st->kern[KC_SMALL].runs += small_runs;
+  for (int b = 0; b < kBigClasses; ++b) {
+    st->kern[KC_BIG128 + b].rows += c.n_big_rows[b];
+    st->kern[KC_BIG128 + b].runs += c.n_big[b];
+  }
+}
+
+// The call's per-class spans: fold the last iteration's set, then read and clear the totals.
+static int collect_kernel_times(klsh_ctx* ctx, int last_set, klsh_stats* st) {
+  using namespace klsh;
+  hipStream_t s = ctx->stream;
+  if (last_set >= 0) launch_stamp_fold(ctx->kstamp, last_set, s);
+  KLSH_HIP(hipGetLastError());
+  unsigned long long tot[2][KC_COUNT];
+  KLSH_HIP(hipMemcpyAsync(tot[0], ctx->kstamp->ticks, sizeof(tot), hipMemcpyDeviceToHost, s));
+  KLSH_HIP(hipMemsetAsync(ctx->kstamp->ticks, 0, sizeof(tot), s));
+  KLSH_HIP(hipStreamSynchronize(s));
+  static_assert(offsetof(KStampBlock, launches) == offsetof(KStampBlock, ticks) + sizeof(unsigned long long) * KC_COUNT,
+                "ticks and launches are adjacent");
+  for (int k = 0; k < KC_COUNT; ++k) {
+    st->kern[k].ms += (double)tot[0][k] * 1e-5;  // 100 MHz ticks
+    st->kern[k].launches += tot[1][k];
+  }
+  return 0;
+}
+
 namespace klsh {
 int ctx_device(const klsh_ctx* ctx) { return ctx->device; }
 hipStream_t ctx_stream(const klsh_ctx* ctx) { return ctx->stream; }
@@ -493,8 +569,13 @@ klsh_ctx* klsh_create(int device, int* err) {
   for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
   for (auto& e : c->sev) ok = ok && hipEventCreate(&e) == hipSuccess;
   for (int i = 0; i < klsh::kMergeStreams; ++i) {
+#ifdef KLSH_AUX1_HI  // A/B: the 65..192-row stream at the high priority too
+    const bool hi = i <= 1;
+#else
+    const bool hi = i == 0;
+#endif
     ok = ok && hipStreamCreateWithPriority(&c->mw.aux[i], hipStreamNonBlocking,
-                                           (i == 0 && big_prio) ? prio_hi : prio_lo) == hipSuccess;
+                                           (hi && big_prio) ? prio_hi : prio_lo) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&c->mw.join[i], hipEventDisableTiming) == hipSuccess;
   }
   ok = ok && hipEventCreateWithFlags(&c->mw.fork, hipEventDisableTiming) == hipSuccess;
@@ -699,23 +780,29 @@ int klsh_restore(klsh_ctx* ctx) {
 // Merge + compaction of one iteration's sorted runs (fk/fv, n positions, in place on fv) into
 // `out` (with ctx->mw.dlist set, the merge kernels also list the survivors they rewrote).
 // Ends with the counters on the host: total (survivors), n_over (oversize runs), n_delta.
+// kt: the iteration's stamps (kNoTime: untimed).
 static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
                       int bucket_thr, uint32_t* out, klsh_stats* st, bool timed,
-                      bool sync = true, const std::function<int(uint32_t*)>* after = nullptr) {
+                      bool sync = true, const std::function<int(uint32_t*)>* after = nullptr,
+                      klsh::KTime kt = klsh::kNoTime) {
   hipStream_t s = ctx->stream;
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
-  // the small-run merge is a launch of its own at >= 2^20 positions (register widths): time it
-  const bool time_small = st && sync && !ctx->comm && n >= (1u << 20) &&
+  // the small-run merge is a launch of its own at >= 2^20 positions (register widths): its HIP
+  // events are the headline's cross-check
+  const bool time_small = kt.blk && st && sync && n >= (1u << 20) &&
                           klsh::project_device_n_ok(ctx->d);
   ctx->mw.small_ev[0] = time_small ? ctx->sev[0] : nullptr;
   ctx->mw.small_ev[1] = time_small ? ctx->sev[1] : nullptr;
+  ctx->mw.kt = kt;
   klsh::launch_merge(ctx->rows, fk, fv, 0, n, thr, bucket_thr, ctx->mw, ctx->ctr, s);
+  ctx->mw.kt = klsh::kNoTime;
   ctx->mw.small_ev[0] = ctx->mw.small_ev[1] = nullptr;
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[3], s));
   const bool zc = sync && ctx->zero_copy;
   klsh::Publish pub{ctx->pub_dev, ctx->pub_seq_dev, ++ctx->pub_seq, ctx->n_next_dev};
-  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s, zc ? &pub : nullptr, ctx->rc);
+  klsh::launch_compact(fv, n, out, ctx->tile_sums, ctx->ctr, s, zc ? &pub : nullptr, ctx->rc, kt,
+                       ctx->lb.status ? &ctx->lb : nullptr);
   KLSH_HIP(hipGetLastError());
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[4], s));
   if (zc && after)  // work queued behind the compaction before the host waits for it
@@ -727,6 +814,10 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   } else {
     ctx->ctr_clean = false;
     if (int e = ctx->sync_counters()) return e;
+  }
+  if (kt.blk && st) {  // this iteration's rows per kernel class
+    const bool tail = n < (1u << 20) && klsh::project_device_n_ok(ctx->d);
+    count_class_rows(st, *ctx->h_ctr, n, tail);
   }
   if (time_small) {  // the compaction (published) runs after the merge streams' join
     KLSH_HIP(hipEventSynchronize(ctx->sev[1]));
@@ -799,9 +890,11 @@ static int merge_nested(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, f
 static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, float thr,
                              int bucket_thr, uint32_t seed_base, uint64_t* rng_counter,
                              klsh_stats* st, bool timed,
-                             const std::function<int(uint32_t*)>* after = nullptr) {
+                             const std::function<int(uint32_t*)>* after = nullptr,
+                             klsh::KTime kt = klsh::kNoTime) {
   uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
-  if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, st, timed, true, after)) return e;
+  if (int e = merge_main(ctx, fk, fv, n, thr, bucket_thr, out, st, timed, true, after, kt))
+    return e;
   // many 385..896-row runs this iteration: the next one runs that class on an auxiliary stream
   ctx->mw.big896_aux = ctx->h_ctr->n_big[klsh::kBigClasses - 1] >= 64u ? 1u : 0u;
   if (ctx->h_ctr->n_over > 0) {
@@ -826,6 +919,16 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     const char* e = getenv("KLSH_ITER_LOG");
     return e ? fopen(e, "a") : nullptr;
   }();
+  // per-class timing: iteration `it` uses set it & 1 (its queued projection included); the
+  // previous iteration's set is read once this one's work is queued
+  // per-class stamps: the call's iterations stamp sets 0, 1, 0, ... in turn (ctx->kt_iter); a
+  // projection first folds the set of the iteration before it
+  const uint64_t kt_first = ctx->kt_iter;
+  auto ktime = [&](uint64_t j) -> klsh::KTime {
+    if (!ctx->kernel_timing || !st) return klsh::kNoTime;
+    if (!ctx->kstamp) return klsh::kNoTime;
+    return klsh::KTime{ctx->kstamp, (int)(j & 1u), j > kt_first ? (int)((j - 1) & 1u) : -1};
+  };
   for (int it = it_begin; it < it_end; ++it) {
     const uint64_t n = ctx->n_live;
     const double t_it = iter_log ? now_ms() : 0.0;
@@ -844,20 +947,23 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     // the projection: queued by the previous iteration (device-side N), or now
     const bool queued = ctx->spec_pending;
     ctx->spec_pending = false;
+    const uint64_t j = ctx->kt_iter++;  // this iteration's stamp set
     if (queued && ctx->spec_k != k) return fail(KLSH_E_STATE, "queued projection out of step");
     const int e0 = queued ? ctx->spec_ev : 0;
+    // the projection runs alone on the main stream: an event pair times it (beside its stamps)
+    const bool rec = true;
     if (!queued) {
       if (!ctx->ctr_clean) if (int e = ctx->reset_counters()) return e;
-      KLSH_HIP(hipEventRecord(ctx->ev[e0], s));
+      if (rec) KLSH_HIP(hipEventRecord(ctx->ev[e0], s));
       klsh::launch_project(ctx->rows, ctx->order, ctx->keys, (uint32_t)n, ctx->hyperplane_ptr(k), h,
-                           0u, s, &ctx->pw);
+                           0u, s, &ctx->pw, ktime(j));
       KLSH_HIP(hipGetLastError());
-      KLSH_HIP(hipEventRecord(ctx->ev[e0 + 1], s));
+      if (rec) KLSH_HIP(hipEventRecord(ctx->ev[e0 + 1], s));
     }
     ctx->ctr_clean = false;
     uint32_t *fk = nullptr, *fv = nullptr;
     klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n, h, ctx->hist,
-                     &fk, &fv, s);
+                     &fk, &fv, s, ktime(j));
     KLSH_HIP(hipGetLastError());
     if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[5], s));
     if (const char* path = getenv("KLSH_BUCKET_STATS")) {  // diagnostics: run-length histogram
@@ -899,11 +1005,11 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
       const uint64_t k_next = k + (uint64_t)h;  // h_next <= h: inside the drawn window
       if (int e = ctx->ensure_hyperplanes(seed_base, k_next, (uint64_t)h, &st->host_ms)) return e;
       const int ne = e0 == 0 ? 6 : 0;
-      KLSH_HIP(hipEventRecord(ctx->ev[ne], s));
+      if (rec) KLSH_HIP(hipEventRecord(ctx->ev[ne], s));
       klsh::launch_project_device_n(ctx->rows, next_order, ctx->keys, (uint32_t)n,
-                                    ctx->hyperplane_ptr(k_next), ctx->n_next_dev, s);
+                                    ctx->hyperplane_ptr(k_next), ctx->n_next_dev, s, ktime(j + 1));
       KLSH_HIP(hipGetLastError());
-      KLSH_HIP(hipEventRecord(ctx->ev[ne + 1], s));
+      if (rec) KLSH_HIP(hipEventRecord(ctx->ev[ne + 1], s));
       ctx->spec_pending = true;
       ctx->spec_k = k_next;
       ctx->spec_ev = ne;
@@ -911,11 +1017,11 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     };
     if (int e = merge_and_compact(ctx, fk, fv, (uint32_t)n, threshold, bucket_size_threshold,
                                   seed_base, rng_counter, st, ctx->phase_timing,
-                                  ahead ? &queue_next : nullptr))
+                                  ahead ? &queue_next : nullptr, ktime(j)))
       return e;
     if (ctx->spec_pending && *rng_counter != ctx->spec_k) ctx->spec_pending = false;  // nested ran
-    st->project_ms += elapsed(ctx->ev[e0], ctx->ev[e0 + 1]);
-    if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
+    if (rec) st->project_ms += elapsed(ctx->ev[e0], ctx->ev[e0 + 1]);
+    if (rec && ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
     st->project_launches += 1;
     st->sum_rows += n;
     st->sum_proj_bits += n * (uint64_t)h;
@@ -927,6 +1033,8 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
               ctx->h_ctr->n_big[2] + ctx->h_ctr->n_big[3], ctx->h_ctr->n_huge);
   }
   if (iter_log) fflush(iter_log);
+  if (ctx->kernel_timing && ctx->kstamp && st && ctx->kt_iter > kt_first)  // per-class spans
+    if (int e = collect_kernel_times(ctx, (int)((ctx->kt_iter - 1) & 1u), st)) return e;
   return 0;
 }
 
@@ -1037,7 +1145,7 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
       return comm_fail("bin histogram allgather");
     klsh::launch_bin_split(ctx->bins_all, W, nbins, N, ctx->owner, ctx->cntmat, s);
     KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->cntmat, 4ull * W * W, hipMemcpyDeviceToHost, s));
-    KLSH_HIP(hipStreamSynchronize(s));
+    if (timed_comm([&] { return cm->wait(s); })) return comm_fail("send counts");
     uint32_t m_g = 0;
     for (int r = 0; r < W; ++r) {
       scnt[r] = 8ull * ctx->h_small[g * W + r];
@@ -1082,7 +1190,7 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
       return comm_fail("counter allgather");
     KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->small, 16ull * W, hipMemcpyDeviceToHost, s));
     KLSH_HIP(hipMemcpyAsync(ctx->h_ctr, ctx->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-    KLSH_HIP(hipStreamSynchronize(s));
+    if (timed_comm([&] { return cm->wait(s); })) return comm_fail("counters");
     if (int e = ctx->check_device_err()) return e;
     if (ctx->phase_timing && st) {
       st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
@@ -1106,7 +1214,7 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
         if (timed_comm([&] { return cm->allgather(ctx->small + 4 * W, ctx->small, 16, s); }))
           return comm_fail("counter allgather");
         KLSH_HIP(hipMemcpyAsync(hs, ctx->small, 16ull * W, hipMemcpyDeviceToHost, s));
-        KLSH_HIP(hipStreamSynchronize(s));
+        if (timed_comm([&] { return cm->wait(s); })) return comm_fail("counter exchange");
         return 0;
       };
       if (int e = exchange_counters((uint32_t)my_hyp, 0, 0, 0)) return e;
@@ -1180,7 +1288,7 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
   }
   if (timed_comm([&] { return cm->allreduce_min_u32(ctx->rows.nxt, ctx->members, s); }))
     return comm_fail("member link allreduce");
-  KLSH_HIP(hipStreamSynchronize(s));
+  if (timed_comm([&] { return cm->wait(s); })) return comm_fail("member link allreduce");
   ctx->n_live = N;
   st->n_final = N;
   st->comm_ms = t_comm;
@@ -1300,6 +1408,10 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   }
   if (n == "phase_timing") {
     ctx->phase_timing = value != 0;
+    return 0;
+  }
+  if (n == "kernel_timing") {
+    ctx->kernel_timing = value != 0;
     return 0;
   }
   if (n == "hyperplane_window") {

@@ -700,6 +700,7 @@ int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* ks, const char* in_path,
     uint8_t* hflag = nullptr;
     uint64_t cap_b = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t done = nullptr;  // after the flag copy: finish() waits for this batch only
     uint64_t n = 0;
   } slot[2];
   int rc = KLSH_OK;
@@ -712,6 +713,7 @@ int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* ks, const char* in_path,
       if (sl.hflag) (void)hipHostFree(sl.hflag);
       if (sl.e0) (void)hipEventDestroy(sl.e0);
       if (sl.e1) (void)hipEventDestroy(sl.e1);
+      if (sl.done) (void)hipEventDestroy(sl.done);
     }
   };
   for (auto& sl : slot) {
@@ -719,7 +721,8 @@ int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* ks, const char* in_path,
               hipMalloc((void**)&sl.dhit, kReads * 4) == hipSuccess &&
               hipMalloc((void**)&sl.dflag, kReads) == hipSuccess &&
               hipHostMalloc((void**)&sl.hflag, kReads, hipHostMallocDefault) == hipSuccess &&
-              hipEventCreate(&sl.e0) == hipSuccess && hipEventCreate(&sl.e1) == hipSuccess;
+              hipEventCreate(&sl.e0) == hipSuccess && hipEventCreate(&sl.e1) == hipSuccess &&
+              hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
       cleanup();
       fclose(of);
@@ -750,6 +753,7 @@ int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* ks, const char* in_path,
     KLSH_XHIP(hipGetLastError());
     KLSH_XHIP(hipEventRecord(sl.e1, s));
     KLSH_XHIP(hipMemcpyAsync(sl.hflag, sl.dflag, sl.n, hipMemcpyDeviceToHost, s));
+    KLSH_XHIP(hipEventRecord(sl.done, s));
     return KLSH_OK;
   };
   auto finish = [&](int si) -> int {
@@ -759,7 +763,9 @@ int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* ks, const char* in_path,
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, sl.e0, sl.e1);
     local.kernel_ms += ms;
-    KLSH_XHIP(hipStreamSynchronize(s));  // the flag copy behind the kernel
+    // the flag copy behind this batch's kernel — not the stream, which by now also holds the next
+    // batch: waiting for that would serialise the host parse behind every kernel
+    KLSH_XHIP(hipEventSynchronize(sl.done));
     out.clear();
     for (uint64_t i = 0; i < sl.n; ++i) {
       const uint64_t len = b.seq_off[i + 1] - b.seq_off[i];

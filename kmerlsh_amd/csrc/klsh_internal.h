@@ -2,6 +2,7 @@
 // (klsh_kernels.hip).  Not part of the C ABI.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -49,11 +50,12 @@ struct alignas(128) CountLine {
 };
 struct RunCounters {
   CountLine n_seg, n_cls[kGroupClasses], n_big[kBigClasses], n_huge, n_over, n_small_rows;
+  CountLine n_big_rows[kBigClasses], n_huge_rows;  // rows in the big / huge runs (kernel rooflines)
 };
 
-// Run-finding workspace (u32 words) for `slots` positions: 13 counts + a tail end + a 4096-bit
+// Run-finding workspace (u32 words) for `slots` positions: 19 counts + a tail end + a 4096-bit
 // head bitmap per 4096-position tile.
-inline uint64_t run_ws_words(uint64_t slots) { return (slots / 4096 + 2) * (14 + 1 + 128) + 64; }
+inline uint64_t run_ws_words(uint64_t slots) { return (slots / 4096 + 2) * (19 + 1 + 128) + 64; }
 
 // Device-side per-iteration counters (zeroed by the host before each iteration).
 struct Counters {
@@ -66,7 +68,47 @@ struct Counters {
   uint32_t n_delta;                // sharded loop: survivors rewritten by a merge this iteration
   uint32_t err;                    // a device-side protocol failure (look-back wait limit); 0 = ok
   uint32_t n_small_rows;           // rows in the runs of 2..64 rows (the small-run merge's rows)
+  uint32_t n_big_rows[kBigClasses];  // rows in the runs of each big class
+  uint32_t n_huge_rows;            // rows in the runs of k_merge_huge
 };
+
+// Per-kernel-class timing (bench.py's roofline) from in-kernel stamps: every workgroup of a timed
+// launch stamps the 100 MHz real-time counter (s_memrealtime) at its start (atomicMin) and at its
+// end (atomicMax) into one of kStampSlots lines of its class, so a class's span in an iteration is
+// first workgroup start -> last workgroup end — the span rocprofv3's kernel trace reports — with
+// no marker packets in the streams.  (HIP event pairs measure from the moment a stream reaches a
+// kernel, resource waits included: tools/ubench_events shows a 50-us kernel timed at 550 us behind
+// a chip-filling kernel of another stream, and event pairs around every merge class added 13-20
+// ms to a C2 step.)  Iteration t stamps set t & 1; the first workgroup of iteration t+1's
+// projection folds set t into the per-class totals (iteration t is complete by then: stream
+// order) and clears it; the engine folds the last set at the end of a call.
+enum KClass : int {
+  KC_PROJECT = 0, KC_SORT, KC_RUNS, KC_SMALL, KC_BIG128, KC_BIG192, KC_BIG384, KC_BIG896, KC_HUGE,
+  KC_TAIL, KC_COMPACT, KC_COUNT
+};
+constexpr int kStampSlots = 16;
+struct alignas(128) StampLine {
+  unsigned long long v;
+  unsigned long long pad_[15];
+};
+struct KStampSet {
+  StampLine t0[KC_COUNT][kStampSlots];  // earliest workgroup start (~0 = none)
+  StampLine t1[KC_COUNT][kStampSlots];  // latest workgroup end (0 = none)
+};
+struct KStampBlock {
+  KStampSet set[2];
+  unsigned long long ticks[KC_COUNT];  // summed spans (10 ns ticks)
+  unsigned long long launches[KC_COUNT];
+};
+// What a launch carries (by value): blk == nullptr = untimed; set = the set it stamps; fold >= 0:
+// the projection folds that set first (the previous iteration's).
+struct KTime {
+  KStampBlock* blk;
+  int set;
+  int fold;
+};
+constexpr KTime kNoTime{nullptr, 0, -1};
+// Fold set `t` into the totals and clear it (one workgroup; device code, klsh_device.cuh).
 
 // Merge workspace (device), sized for `cap` positions.
 struct MergeWork {
@@ -90,7 +132,8 @@ struct MergeWork {
   // the engine when the previous iteration had many of them (C4: thousands; C2: < 10)
   uint32_t big896_aux;
   hipStream_t aux[3];
-  hipEvent_t small_ev[2];  // timing events around the small-run launch (nullptr: not recorded)
+  KTime kt;                // per-class stamps of this iteration's merge launches
+  hipEvent_t small_ev[2];  // HIP events around the small-run launch (nullptr: not recorded)
   hipEvent_t fork;
   hipEvent_t join[3];
 };
@@ -146,17 +189,19 @@ struct ProjectWork {
 // d in {8, 16, 32, 64} (project_device_n_ok).
 bool project_device_n_ok(int d);
 void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n_max,
-                             const float* W, const uint32_t* n_dev, hipStream_t s);
+                             const float* W, const uint32_t* n_dev, hipStream_t s,
+                             KTime kt = kNoTime);
 
 // pw (may be null): the workspace that enables the matrix-core kernel for wide rows (d > 64).
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
                     const float* W, int h, uint32_t key_or, hipStream_t s,
-                    const ProjectWork* pw = nullptr);
+                    const ProjectWork* pw = nullptr, KTime kt = kNoTime);
 
 // Stable LSD radix sort of (keys, vals)[0..n) on the low `bits` bits (klsh_sort.hip); ping-pong
 // buffers, *out_k/*out_v = the pair holding the result.  ws: sort_ws_words(n) words.
 void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
-                uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s);
+                uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s,
+                KTime kt = kNoTime);
 
 // Greedy merge (p_cluster) over every bucket run of equal key in positions [lo, hi) of
 // (key, slots), in place: survivors first in each run, kInvalid after.  Runs longer than
@@ -174,11 +219,22 @@ struct Publish {
   uint32_t* n_next;   // device word that also receives the survivor count (may be null)
 };
 
+// The look-back compaction's tile status words (>= 256, zeroed once) and the epoch of its last
+// launch (status words carry the epoch, so they are never cleared).
+struct LookBack {
+  unsigned long long* status;
+  mutable uint32_t epoch;
+};
+
 // out[0..total) = slots[p] for p with slots[p] != kInvalid, stable; ctr->total = count.  rc (may
-// be null): the iteration's run counters, copied into *ctr (and zeroed) before the publish.
+// be null): the iteration's run counters, copied into *ctr (and zeroed) before the publish.  lb
+// (may be null): one launch instead of two when n fits 256 tiles.
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
                     Counters* ctr, hipStream_t s, const Publish* pub = nullptr,
-                    RunCounters* rc = nullptr);
+                    RunCounters* rc = nullptr, KTime kt = kNoTime,
+                    const LookBack* lb = nullptr);
+// Fold set `set` of blk into its totals and clear it (the end of a timed call).
+void launch_stamp_fold(KStampBlock* blk, int set, hipStream_t s);
 
 // Mode-C producer: rows x[i] (slot i) from counts (d x bs, sample-major), LUT ln(c+1),
 // v_kmers; order[] = kept rows (sum > 0.1 d) compacted; ctr->total = kept count.

@@ -60,9 +60,12 @@ __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X,
                                                     uint32_t* __restrict__ keys, uint32_t n,
                                                     const float* __restrict__ W, int h,
                                                     uint32_t key_or,
-                                                    const uint32_t* __restrict__ n_dev = nullptr) {
+                                                    const uint32_t* __restrict__ n_dev = nullptr,
+                                                    KTime kt = kNoTime) {
   constexpr int QMAX = kMaxHyperplanes / 4;
   __shared__ __attribute__((aligned(16))) float4 sw[QMAX * D];
+  kt_fold(kt);
+  kt_begin(kt, KC_PROJECT);
   if (n_dev) {
     n = *n_dev;
     if (n == 0) return;
@@ -137,6 +140,7 @@ __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X,
     const uint32_t pr = p0 + 256u * r;
     if (pr < n) keys[pr] = (key[r] >> (uint32_t)(4 * nq - h)) | key_or;  // drop padding bits
   }
+  kt_end(kt, KC_PROJECT);
 }
 
 // Wide rows (d > 64 or any width without a register kernel), packed f32: every lane keeps the
@@ -148,9 +152,11 @@ __global__ __launch_bounds__(256) void k_project_wide_pk(const float* __restrict
                                                          int dp, const uint32_t* __restrict__ slots,
                                                          uint32_t* __restrict__ keys, uint32_t n,
                                                          const float* __restrict__ W, int h,
-                                                         uint32_t key_or) {
+                                                         uint32_t key_or, KTime kt) {
   extern __shared__ __attribute__((aligned(16))) float4 swq[];  // [dp][nq]
   constexpr int QMAX = kMaxHyperplanes / 4;
+  kt_fold(kt);
+  kt_begin(kt, KC_PROJECT);
   const int nq = (h + 3) >> 2;
   for (int i = threadIdx.x; i < dp * nq; i += 256) {
     const int k = i / nq, q = i % nq;
@@ -225,6 +231,7 @@ __global__ __launch_bounds__(256) void k_project_wide_pk(const float* __restrict
     const uint32_t pr = p0 + 256u * r;
     if (pr < n) keys[pr] = (key >> (uint32_t)(4 * nq - h)) | key_or;
   }
+  kt_end(kt, KC_PROJECT);
 }
 
 // Any d: 32 running sums in registers (unrolled, predicated on the wave-uniform h), the row
@@ -233,7 +240,9 @@ __global__ __launch_bounds__(256) void k_project_generic(const float* __restrict
                                                          int dp, const uint32_t* __restrict__ slots,
                                                          uint32_t* __restrict__ keys, uint32_t n,
                                                          const float* __restrict__ W, int h,
-                                                         uint32_t key_or) {
+                                                         uint32_t key_or, KTime kt) {
+  kt_fold(kt);
+  kt_begin(kt, KC_PROJECT);
   const uint32_t p = blockIdx.x * 256u + threadIdx.x;
   if (p >= n) return;
   const float* x = X + (size_t)slots[p] * dp;
@@ -265,6 +274,7 @@ __global__ __launch_bounds__(256) void k_project_generic(const float* __restrict
   for (int j = 0; j < kMaxHyperplanes; ++j)
     if (j < h) key = key * 2u + (s[j] >= 0.0f ? 1u : 0u);
   keys[p] = key | key_or;
+  kt_end(kt, KC_PROJECT);
 }
 
 // Matrix-core projection, certified.  S = X W^T for 32 rows x 32 hyperplanes per wave with the
@@ -420,8 +430,11 @@ __global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __re
                                                            const uint32_t* __restrict__ slots,
                                                            uint32_t* __restrict__ keys, uint32_t n,
                                                            const float* __restrict__ W, int h,
-                                                           uint32_t key_or, float eps, ProjectWork pw) {
+                                                           uint32_t key_or, float eps, ProjectWork pw,
+                                                           KTime kt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+  kt_fold(kt);
+  kt_begin(kt, KC_PROJECT);
   const int KS = (d + 15) / 16;
   pbf16x8* bfr = reinterpret_cast<pbf16x8*>(psm);  // [KS][64 lanes][hi, lo]
   float* swn = reinterpret_cast<float*>(psm + (size_t)KS * 64 * 2 * sizeof(pbf16x8));  // [32]
@@ -551,7 +564,7 @@ __global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X
                                                      const uint32_t* __restrict__ slots,
                                                      uint32_t* __restrict__ keys,
                                                      const float* __restrict__ W, int h,
-                                                     ProjectWork pw) {
+                                                     ProjectWork pw, KTime kt) {
   extern __shared__ __attribute__((aligned(16))) float fw[];  // the h hyperplanes, stride dp
   __shared__ uint32_t s_last;
   const uint32_t count = min(pw.ws[0], pw.cap);
@@ -588,6 +601,7 @@ __global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X
     atomicExch(&pw.ws[0], 0u);
     atomicExch(&pw.ws[1], 0u);
   }
+  kt_end(kt, KC_PROJECT);  // the screen + fix-up span (k_project_mfma_wide stamps the start)
 }
 
 bool project_device_n_ok(int d) {
@@ -595,14 +609,17 @@ bool project_device_n_ok(int d) {
 }
 
 void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n_max,
-                             const float* W, const uint32_t* n_dev, hipStream_t s) {
+                             const float* W, const uint32_t* n_dev, hipStream_t s, KTime kt) {
   if (n_max == 0) return;
   const dim3 grid((n_max + 255) / 256), block(256);
+  auto go = [&](auto kern) {
+    kern<<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev, kt);
+  };
   switch (r.d) {
-    case 8: k_project_pk<8, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev); break;
-    case 16: k_project_pk<16, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev); break;
-    case 32: k_project_pk<32, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev); break;
-    default: k_project_pk<64, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev); break;
+    case 8: go(k_project_pk<8, 2, 1>); break;
+    case 16: go(k_project_pk<16, 2, 1>); break;
+    case 32: go(k_project_pk<32, 2, 1>); break;
+    default: go(k_project_pk<64, 2, 1>); break;
   }
 }
 
@@ -620,7 +637,8 @@ static bool project_mfma_requested() {
 }
 
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
-                    const float* W, int h, uint32_t key_or, hipStream_t s, const ProjectWork* pw) {
+                    const float* W, int h, uint32_t key_or, hipStream_t s, const ProjectWork* pw,
+                    KTime kt) {
   if (n == 0) return;
   const dim3 grid((n + 255) / 256), block(256);
   if (pw && r.d > 64 && h > 0) {
@@ -635,9 +653,12 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
       (void)lds_ok;
       const uint32_t groups = (n + kWideNT / 2 - 1) / (kWideNT / 2);  // 32 rows per wave
       const dim3 gm(std::min<uint32_t>(groups, 2048u));
-      k_project_mfma_wide<<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or,
-                                                 project_eps(r.d), *pw);
-      k_project_fix<<<1024, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw);
+      // stamped as one span: the screen (start) and the fix-up of its close calls (end)
+      KTime k1 = kt;
+      k1.fold = -1;
+      k_project_mfma_wide<<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h,
+                                                         key_or, project_eps(r.d), *pw, kt);
+      k_project_fix<<<1024, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
       return;
     }
   }
@@ -645,16 +666,22 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
     const uint32_t groups = (n + 127) / 128;  // 4 waves x 32 rows per workgroup per step
     const dim3 gm(std::min<uint32_t>(groups, 8192u));
     const float eps = project_eps(r.d);
-    if (r.d == 64) k_project_mfma<64><<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
-    else if (r.d == 32) k_project_mfma<32><<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
-    else k_project_mfma<16><<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
+    auto go = [&](auto kern) {  // (diagnostic variant: not stamped)
+      kern<<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
+    };
+    if (r.d == 64) go(k_project_mfma<64>);
+    else if (r.d == 32) go(k_project_mfma<32>);
+    else go(k_project_mfma<16>);
     return;
   }
+  auto go_pk = [&](auto kern) {
+    kern<<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, nullptr, kt);
+  };
   switch (r.d) {
-    case 8: k_project_pk<8, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
-    case 16: k_project_pk<16, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
-    case 32: k_project_pk<32, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
-    case 64: k_project_pk<64, 2, 1><<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or); break;
+    case 8: go_pk(k_project_pk<8, 2, 1>); break;
+    case 16: go_pk(k_project_pk<16, 2, 1>); break;
+    case 32: go_pk(k_project_pk<32, 2, 1>); break;
+    case 64: go_pk(k_project_pk<64, 2, 1>); break;
     default: {
       const size_t lds = sizeof(float4) * (size_t)r.dp * (size_t)((h + 3) / 4);
       if (lds <= 64 * 1024) {
@@ -662,9 +689,10 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
             hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_wide_pk<1>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;
         (void)lds_ok;
-        k_project_wide_pk<1><<<grid, block, lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or);
+        k_project_wide_pk<1><<<grid, block, lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or,
+                                                      kt);
       } else {
-        k_project_generic<<<grid, block, 0, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or);
+        k_project_generic<<<grid, block, 0, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h, key_or, kt);
       }
     }
   }
@@ -677,8 +705,10 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
 // contiguous per wave (the generic scan reads and writes 16 consecutive items per lane).
 constexpr int kCompactTile = 4096;
 __global__ __launch_bounds__(256) void k_compact_count(const uint32_t* __restrict__ slots,
-                                                       uint32_t n, uint32_t* __restrict__ counts) {
+                                                       uint32_t n, uint32_t* __restrict__ counts,
+                                                       KTime kt) {
   __shared__ uint32_t wsum[4];
+  kt_begin(kt, KC_COMPACT);
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t T0 = blockIdx.x * (uint32_t)kCompactTile;
   uint32_t c = 0;
@@ -713,6 +743,13 @@ __device__ __forceinline__ void collect_run_counts(Counters* ctr, RunCounters* r
   rc->n_over.v = 0u;
   ctr->n_small_rows = rc->n_small_rows.v;
   rc->n_small_rows.v = 0u;
+#pragma unroll
+  for (int c = 0; c < kBigClasses; ++c) {
+    ctr->n_big_rows[c] = rc->n_big_rows[c].v;
+    rc->n_big_rows[c].v = 0u;
+  }
+  ctr->n_huge_rows = rc->n_huge_rows.v;
+  rc->n_huge_rows.v = 0u;
 }
 
 // Publish the iteration's counters to the host (see Publish), `total` filled in.
@@ -741,7 +778,7 @@ __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restric
                                                        uint32_t* __restrict__ out,
                                                        uint32_t* __restrict__ total,
                                                        Counters* ctr, Publish pub,
-                                                       RunCounters* rc) {
+                                                       RunCounters* rc, KTime kt) {
   constexpr int K = kCompactTile / 256;
   __shared__ uint32_t cnt[K * 4], pre[K * 4 + 1], wsum[4];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -780,10 +817,85 @@ __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restric
     collect_run_counts(ctr, rc);
     if (pub.host) publish_counters(ctr, pre[K * 4], pub);
   }
+  kt_end(kt, KC_COMPACT);
+}
+
+// Small iterations (<= 256 tiles, every tile resident at once): the same compaction in ONE launch
+// with a look-back — a tile publishes its survivor count (tagged with the launch's epoch) right
+// after counting, then sums the counts of the tiles before it (thread j waits for tile j's word;
+// a predecessor publishes before it waits for anyone, so the waits cannot cycle).  One dependent
+// launch less per iteration.  A wait that exceeds its bound sets ctr->err (reported, not hung).
+__global__ __launch_bounds__(256) void k_compact_lb(const uint32_t* __restrict__ slots, uint32_t n,
+                                                    uint32_t* __restrict__ out,
+                                                    unsigned long long* __restrict__ status,
+                                                    uint32_t epoch, uint32_t* __restrict__ total,
+                                                    Counters* ctr, Publish pub, RunCounters* rc,
+                                                    KTime kt) {
+  constexpr int K = kCompactTile / 256;
+  __shared__ uint32_t cnt[K * 4], pre[K * 4 + 1], wsum[4];
+  kt_begin(kt, KC_COMPACT);
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t T0 = blockIdx.x * (uint32_t)kCompactTile;
+  uint32_t v[K];
+  uint64_t m[K];
+  uint32_t mine = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t i = T0 + k * 256u + t;
+    v[k] = i < n ? slots[i] : kInvalid;
+    m[k] = __ballot(v[k] != kInvalid);
+    mine += (uint32_t)__popcll(m[k]);
+    if (lane == 0) cnt[k * 4 + wv] = (uint32_t)__popcll(m[k]);
+  }
+  if (lane == 0) wsum[wv] = mine;
+  __syncthreads();
+  if (t == 0)
+    __hip_atomic_store(&status[blockIdx.x],
+                       ((unsigned long long)epoch << 32) | (wsum[0] + wsum[1] + wsum[2] + wsum[3]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t before = 0;
+  if (t < blockIdx.x) {
+    unsigned long long w = 0;
+    for (uint32_t spin = 0;; ++spin) {
+      w = __hip_atomic_load(&status[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(w >> 32) == epoch) break;
+      if (spin > (1u << 24)) {  // a protocol failure: report it instead of hanging
+        atomicOr(&ctr->err, 4u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    before = (uint32_t)w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+  __syncthreads();  // wsum is rewritten below
+  if (lane == 0) wsum[wv] = before;
+  __syncthreads();
+  if (t == 0) {  // offsets of the (row k, wave w) groups in position order
+    uint32_t a = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    for (int q = 0; q < K * 4; ++q) {
+      pre[q] = a;
+      a += cnt[q];
+    }
+    pre[K * 4] = a;
+  }
+  __syncthreads();
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (v[k] != kInvalid) out[pre[k * 4 + wv] + (uint32_t)__popcll(m[k] & below)] = v[k];
+  if (blockIdx.x == gridDim.x - 1 && t == 0) {
+    *total = pre[K * 4];
+    collect_run_counts(ctr, rc);
+    if (pub.host) publish_counters(ctr, pre[K * 4], pub);
+  }
+  kt_end(kt, KC_COMPACT);
 }
 
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
-                    Counters* ctr, hipStream_t s, const Publish* pub, RunCounters* rc) {
+                    Counters* ctr, hipStream_t s, const Publish* pub, RunCounters* rc, KTime kt,
+                    const LookBack* lb) {
   const Publish none{nullptr, nullptr, 0u, nullptr};
   if (n == 0) {
     (void)hipMemsetAsync(&ctr->total, 0, sizeof(uint32_t), s);
@@ -791,10 +903,16 @@ void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* 
     return;
   }
   const uint32_t ntiles = (n + kCompactTile - 1) / kCompactTile;
+  if (lb && lb->status && ntiles <= 256u) {
+    const uint32_t epoch = ++lb->epoch;
+    k_compact_lb<<<ntiles, 256, 0, s>>>(slots, n, out, lb->status, epoch, &ctr->total, ctr,
+                                        pub ? *pub : none, rc, kt);
+    return;
+  }
   uint32_t* counts = tile_sums + kScanSumsWord;
-  k_compact_count<<<ntiles, 256, 0, s>>>(slots, n, counts);
+  k_compact_count<<<ntiles, 256, 0, s>>>(slots, n, counts, kt);
   k_compact_apply<<<ntiles, 256, 0, s>>>(slots, n, counts, out, &ctr->total, ctr, pub ? *pub : none,
-                                         rc);
+                                         rc, kt);
 }
 
 // ============================================================================= mode C =========
@@ -835,6 +953,12 @@ void launch_convert(const Rows& r, const uint16_t* counts, uint32_t bs, const fl
   }
   k_convert<<<(bs + 255) / 256, 256, 0, s>>>(r, counts, bs, lut, v_kmers, keep);
   device_scan(SrcArray{keep}, DstCompactIndex{order}, bs, tile_sums, &ctr->total, &ctr->err, s);
+}
+
+__global__ void k_stamp_fold(KStampBlock* blk, int set) { kt_fold_set(blk, set, threadIdx.x); }
+
+void launch_stamp_fold(KStampBlock* blk, int set, hipStream_t s) {
+  if (blk) k_stamp_fold<<<1, 64, 0, s>>>(blk, set);
 }
 
 // ============================================================================== misc ==========

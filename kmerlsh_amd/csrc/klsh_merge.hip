@@ -566,7 +566,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     MergeWork w, uint32_t* __restrict__ slots,
                                                     Decider dc, Rows r, Counters* ctr) {
   __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
+  kt_begin(w.kt, KC_SMALL);
   small_loop<D>(w, slots, dc, r, ctr, lds, blockIdx.x, gridDim.x);
+  kt_end(w.kt, KC_SMALL);
 }
 
 // Runs of equal keys, listed by size class, in three launches and no contended atomics:
@@ -582,14 +584,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // positional.
 constexpr uint32_t kRunTile = 4096;
 constexpr int kRunLists = kGroupClasses + kBigClasses + 2;  // small classes, big classes, huge, over
-constexpr int kRunRows = kRunLists + 2;  // + the head count (n_seg) + rows in small runs
+// + the head count (n_seg), rows in small runs, rows in each big class and in huge runs
+constexpr int kRunRows = kRunLists + 2 + kBigClasses + 1;
 
 __device__ __forceinline__ uint32_t* run_counter(RunCounters* rc, int l) {
   return l < kGroupClasses ? &rc->n_cls[l].v
          : l < kGroupClasses + kBigClasses ? &rc->n_big[l - kGroupClasses].v
          : l == kRunLists - 2 ? &rc->n_huge.v
          : l == kRunLists - 1 ? &rc->n_over.v
-         : l == kRunLists ? &rc->n_seg.v : &rc->n_small_rows.v;
+         : l == kRunLists ? &rc->n_seg.v
+         : l == kRunLists + 1 ? &rc->n_small_rows.v
+         : l < kRunLists + 2 + kBigClasses ? &rc->n_big_rows[l - kRunLists - 2].v
+                                           : &rc->n_huge_rows.v;
 }
 
 // The run starting at tile-local position q (a head of bitmap hb): its length and list (-1: one row).
@@ -614,7 +620,8 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
                                                     uint32_t n, int bucket_thr, uint32_t ntiles,
                                                     uint64_t* __restrict__ hbits,
                                                     uint32_t* __restrict__ tail_ends,
-                                                    uint32_t* __restrict__ counts) {
+                                                    uint32_t* __restrict__ counts, KTime kt) {
+  kt_begin(kt, KC_RUNS);
   __shared__ uint64_t hb[kRunTile / 64];
   __shared__ uint32_t lcnt[kRunRows];
   __shared__ uint32_t s_tail_end;
@@ -658,6 +665,7 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
   const uint32_t tail_end = s_tail_end;
   const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   uint32_t heads = 0, small_rows = 0;
+  uint32_t lrows[kBigClasses + 1] = {};  // rows per big class, then huge
 #pragma unroll 4
   for (int k = 0; k < 16; ++k) {
     const uint32_t q = (uint32_t)k * 256u + t;
@@ -667,6 +675,9 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
       l = run_list(hb, T0, tail_end, q, bucket_thr, b);
       ++heads;
       if (l >= 0 && l < kGroupClasses) small_rows += b;
+#pragma unroll
+      for (int c = 0; c <= kBigClasses; ++c)
+        if (l == kGroupClasses + c) lrows[c] += b;
     }
     // lanes with the same list: one LDS add by the lowest of them
     const uint32_t id = (uint32_t)(l + 1);  // 0 = no entry
@@ -682,9 +693,14 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
   for (int o = 32; o > 0; o >>= 1) {
     heads += __shfl_xor(heads, o, 64);
     small_rows += __shfl_xor(small_rows, o, 64);
+#pragma unroll
+    for (int c = 0; c <= kBigClasses; ++c) lrows[c] += __shfl_xor(lrows[c], o, 64);
   }
   if (lane == 0 && heads) atomicAdd(&lcnt[kRunLists], heads);
   if (lane == 0 && small_rows) atomicAdd(&lcnt[kRunLists + 1], small_rows);
+#pragma unroll
+  for (int c = 0; c <= kBigClasses; ++c)
+    if (lane == 0 && lrows[c]) atomicAdd(&lcnt[kRunLists + 2 + c], lrows[c]);
   __syncthreads();
   if (t < (uint32_t)kRunRows) counts[(size_t)t * ntiles + blockIdx.x] = lcnt[t];
 }
@@ -708,6 +724,10 @@ __global__ __launch_bounds__(256) void k_runs_scan(uint32_t* __restrict__ counts
   if (t == 0) *run_counter(rc, (int)blockIdx.x) = total;
 }
 
+// SCAN (ntiles <= 256, every iteration below 2^20 positions): `counts` are the raw per-tile counts
+// and each workgroup sums its own list bases (the tiles before it; thread t holds tile t) — and
+// workgroup 0 the list totals — so k_runs_scan is not launched: one dependent launch less.
+template <bool SCAN>
 __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, int bucket_thr, uint32_t ntiles,
                                                     const uint64_t* __restrict__ hbits,
                                                     const uint32_t* __restrict__ tail_ends,
@@ -718,9 +738,38 @@ __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, int bucket_thr,
   const uint32_t t = threadIdx.x;
   const uint32_t T0 = blockIdx.x * kRunTile;
   if (t < kRunTile / 64) hb[t] = hbits[(size_t)blockIdx.x * (kRunTile / 64) + t];
-  if (t < (uint32_t)kRunLists) {
-    lbase[t] = counts[(size_t)t * ntiles + blockIdx.x];
-    lfill[t] = 0u;
+  if constexpr (SCAN) {
+    __shared__ uint32_t red[2][4][kRunRows];
+    const uint32_t lane = t & 63u, wv = t >> 6;
+    uint32_t cv[kRunRows];  // every load in flight before the reductions
+#pragma unroll
+    for (int l = 0; l < kRunRows; ++l) cv[l] = t < ntiles ? counts[(size_t)l * ntiles + t] : 0u;
+#pragma unroll
+    for (int l = 0; l < kRunRows; ++l) {
+      const uint32_t v = cv[l];
+      uint32_t before = t < blockIdx.x ? v : 0u, all = v;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        before += __shfl_xor(before, o, 64);
+        all += __shfl_xor(all, o, 64);
+      }
+      if (lane == 0) {
+        red[0][wv][l] = before;
+        red[1][wv][l] = all;
+      }
+    }
+    __syncthreads();
+    if (t < (uint32_t)kRunLists) {
+      lbase[t] = red[0][0][t] + red[0][1][t] + red[0][2][t] + red[0][3][t];
+      lfill[t] = 0u;
+    }
+    if (blockIdx.x == 0 && t < (uint32_t)kRunRows)
+      *run_counter(w.rc, (int)t) = red[1][0][t] + red[1][1][t] + red[1][2][t] + red[1][3][t];
+  } else {
+    if (t < (uint32_t)kRunLists) {
+      lbase[t] = counts[(size_t)t * ntiles + blockIdx.x];
+      lfill[t] = 0u;
+    }
   }
   __syncthreads();
   const uint32_t tail_end = tail_ends[blockIdx.x];
@@ -739,6 +788,7 @@ __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, int bucket_thr,
       else w.over[at] = e;
     }
   }
+  kt_end(w.kt, KC_RUNS);
 }
 
 // ------------------------------------------------------------------- runs of 65..896 rows -----
@@ -1544,13 +1594,23 @@ template <int D, int RB, int NT, bool ROWS_LDS>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RB <= 192 ? 2 : 1))) void k_merge_big(const uint2* __restrict__ list, int cls,
                                                   uint32_t* __restrict__ slots, Decider dc,
                                                   Rows r, Counters* ctr, uint32_t* dlist,
-                                                  RunCounters* rc) {
+                                                  RunCounters* rc, KTime kt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  kt_begin(kt, KC_BIG128 + cls);
   const uint32_t count =
       __hip_atomic_load(&rc->n_big[cls].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   big_runs<D, RB, NT, ROWS_LDS>(list, cls, count, blockIdx.x, gridDim.x, slots, dc, r, ctr, dlist,
                                 smem);
+  kt_end(kt, KC_BIG128 + cls);
 }
+
+constexpr uint32_t kHugeLdsRows = 8192;  // a huge run's slots and norms in LDS up to this length
+template <int D, int NT>
+__device__ __forceinline__ void huge_runs(const uint2* __restrict__ list, uint32_t count,
+                                          uint32_t first, uint32_t stride,
+                                          uint32_t* __restrict__ slots, const Decider& dc,
+                                          const Rows& r, const MergeWork& w, Counters* ctr,
+                                          unsigned char* smem);
 
 // Small iterations: every merge class in ONE launch on the main stream (no fork/join across
 // streams, ≈35 us per iteration there): workgroups [0, nbig) take the 65..896-row runs (the
@@ -1560,16 +1620,23 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
                                                     Decider dc, Rows r, Counters* ctr,
                                                     uint32_t nbig) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  kt_begin(w.kt, KC_TAIL);
   if (blockIdx.x < nbig) {
     uint32_t cnt[kBigClasses];
 #pragma unroll
     for (int c = 0; c < kBigClasses; ++c)
       cnt[c] = __hip_atomic_load(&w.rc->n_big[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // one index space, longest class first: 385..896, 193..384, 129..192, 65..128
-    const uint32_t a3 = cnt[3], a2 = a3 + cnt[2], a1 = a2 + cnt[1], total = a1 + cnt[0];
+    const uint32_t nh = __hip_atomic_load(&w.rc->n_huge.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // one index space, longest runs first: > 896 (no k_merge_huge launch in these iterations),
+    // 385..896, 193..384, 129..192, 65..128
+    const uint32_t a4 = nh, a3 = a4 + cnt[3], a2 = a3 + cnt[2], a1 = a2 + cnt[1],
+                   total = a1 + cnt[0];
     for (uint32_t li = blockIdx.x; li < total; li += nbig) {  // block-uniform
-      if (li < a3)
-        big_runs<D, 896, 256, false>(w.big[3], 3, li + 1, li, 1u << 30, slots, dc, r, ctr, w.dlist, smem);
+      if (li < a4)
+        huge_runs<D, 256>(w.huge, li + 1, li, 1u << 30, slots, dc, r, w, ctr, smem);
+      else if (li < a3)
+        big_runs<D, 896, 256, false>(w.big[3], 3, li - a4 + 1, li - a4, 1u << 30, slots, dc, r,
+                                     ctr, w.dlist, smem);
       else if (li < a2)
         big_runs<D, 384, 256, true>(w.big[2], 2, li - a3 + 1, li - a3, 1u << 30, slots, dc, r, ctr,
                                     w.dlist, smem);
@@ -1586,6 +1653,7 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
     float* lds = reinterpret_cast<float*>(smem) + wv * 64 * (D + 4);
     small_loop<D>(w, slots, dc, r, ctr, lds, (blockIdx.x - nbig) * 4u + wv, (gridDim.x - nbig) * 4u);
   }
+  kt_end(w.kt, KC_TAIL);
 }
 
 // ------------------------------------------------------ runs longer than 896 rows: workgroups -----
@@ -1595,24 +1663,25 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
 // by a ballot + cross-wave min.  The run's slots and sqrtf(norms) live in LDS when they fit.
 constexpr int kHugeNT = 512;
 constexpr int kHugeKB = 8;  // visited rows tested per pass (half at d = 64); 16 measured the same
-constexpr uint32_t kHugeLdsRows = 8192;
 
-template <int D>  // D: d at compile time (unrolled dots), 0 = any d
-__global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict__ list,
-                                                       const uint32_t* count_ptr,
-                                                       uint32_t* __restrict__ slots, Decider dc,
-                                                       Rows r, MergeWork w, Counters* ctr) {
-  constexpr int NW = kHugeNT / 64;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// The runs li = first, first + stride, ... (< count) of the huge list, one workgroup of NT lanes
+// per run (k_merge_huge: 512 lanes; k_merge_tail's big-run workgroups: 256), smem = huge_lds().
+template <int D, int NT>  // D: d at compile time (unrolled dots), 0 = any d
+__device__ __forceinline__ void huge_runs(const uint2* __restrict__ list, uint32_t count,
+                                          uint32_t first, uint32_t stride,
+                                          uint32_t* __restrict__ slots, const Decider& dc,
+                                          const Rows& r, const MergeWork& w, Counters* ctr,
+                                          unsigned char* smem) {
+  constexpr int NW = NT / 64;
+  constexpr int kHugeNT = NT;  // (the body below is written for any NT)
   uint32_t* ls = reinterpret_cast<uint32_t*>(smem);             // [kHugeLdsRows] slots
   float* lq = reinterpret_cast<float*>(ls + kHugeLdsRows);       // [kHugeLdsRows] sqrtf(nrm)
   float* xi = lq + kHugeLdsRows;                                 // [dp] the visited row
   __shared__ uint32_t wmin[2][NW];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const int d = r.d, dp = r.dp;
-  const uint32_t count = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint32_t par = 0;
-  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+  for (uint32_t li = first; li < count; li += stride) {
     const uint2 e = list[li];
     const uint32_t p = e.x, b = e.y;
     const bool in_lds = b <= kHugeLdsRows;
@@ -1802,14 +1871,31 @@ __global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict_
   }
 }
 
+template <int D>
+__global__ __launch_bounds__(kHugeNT) void k_merge_huge(const uint2* __restrict__ list,
+                                                       const uint32_t* count_ptr,
+                                                       uint32_t* __restrict__ slots, Decider dc,
+                                                       Rows r, MergeWork w, Counters* ctr) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  kt_begin(w.kt, KC_HUGE);
+  const uint32_t count = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  huge_runs<D, kHugeNT>(list, count, blockIdx.x, gridDim.x, slots, dc, r, w, ctr, smem);
+  kt_end(w.kt, KC_HUGE);
+}
+
+// LDS of huge_runs: slots + sqrt norms, then the candidate rows + their norms + per-wave first
+// hits (register widths), or the visited row
+static size_t huge_lds(int d, int dp, int nt) {
+  const bool batched = d == 8 || d == 16 || d == 32 || d == 64;
+  return sizeof(uint32_t) * kHugeLdsRows * 2 +
+         (batched ? sizeof(float) * (size_t)dp * kHugeKB + sizeof(float) * kHugeKB +
+                        sizeof(uint32_t) * kHugeKB * (nt / 64)
+                  : sizeof(float) * (size_t)dp);
+}
+
 static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, const Rows& r,
                         Counters* ctr, uint32_t n, hipStream_t s) {
-  // slots + sqrt norms, then the candidate rows + their norms + per-wave first hits
-  const bool batched = r.d == 8 || r.d == 16 || r.d == 32 || r.d == 64;
-  const size_t lds = sizeof(uint32_t) * kHugeLdsRows * 2 +
-                     (batched ? sizeof(float) * (size_t)r.dp * kHugeKB + sizeof(float) * kHugeKB +
-                                    sizeof(uint32_t) * kHugeKB * (kHugeNT / 64)
-                              : sizeof(float) * (size_t)r.dp);
+  const size_t lds = huge_lds(r.d, r.dp, kHugeNT);
   static const bool lds_ok = [] {
     bool ok = true;
     for (const void* f : {reinterpret_cast<const void*>(&k_merge_huge<0>),
@@ -2017,9 +2103,10 @@ template <int G>
 __global__ __launch_bounds__(64) void k_merge_group_wide(const uint2* __restrict__ list, int cls,
                                                          uint32_t* __restrict__ slots, Decider dc,
                                                          Rows r, Counters* ctr, uint32_t* dlist,
-                                                         RunCounters* rc) {
+                                                         RunCounters* rc, KTime kt) {
   __shared__ __attribute__((aligned(16))) float tile[64 * (kWideKC + 4)];
   constexpr uint32_t NG = 64 / G;
+  kt_begin(kt, KC_SMALL);
   const uint32_t n = __hip_atomic_load(&rc->n_cls[cls].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nb = (n + NG - 1) / NG;
   const uint32_t g = threadIdx.x & (G - 1), grp = threadIdx.x / G;
@@ -2029,6 +2116,7 @@ __global__ __launch_bounds__(64) void k_merge_group_wide(const uint2* __restrict
     const uint32_t slot = g < e.y ? slots[e.x + g] : 0u;
     merge_batch_wide<G>(e.x, e.y, slot, slots, dc, r, tile, dlist, ctr);
   }
+  kt_end(kt, KC_SMALL);
 }
 
 // Runs of 65..896 rows with wide rows: one workgroup per run, the decision matrix in LDS in
@@ -2050,8 +2138,9 @@ template <int RB, int NT, int KC>
 __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__ list, int cls,
                                                        uint32_t* __restrict__ slots, Decider dc,
                                                        Rows r, Counters* ctr, uint32_t* dlist,
-                                                       RunCounters* rc) {
+                                                       RunCounters* rc, KTime kt) {
   using L = BigWideLayout<RB, NT, KC>;
+  kt_begin(kt, KC_BIG128 + cls);
   constexpr int W = L::W, NW = L::NW, STB = L::STB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* P = reinterpret_cast<uint64_t*>(smem + L::P);
@@ -2152,6 +2241,7 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__
                      reinterpret_cast<float*>(smem + L::tiles), wbuf, r, dc, slots, dlist, ctr);
     __syncthreads();
   }
+  kt_end(kt, KC_BIG128 + cls);
 }
 
 // ----------------------------------------------------------------------------- launch -----
@@ -2208,7 +2298,7 @@ static void launch_big(const MergeWork& w, int c, uint32_t* slots, const Decider
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
   const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
   k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist,
-                                                           w.rc);
+                                                           w.rc, w.kt);
 }
 
 // Fork the size-class kernels onto the auxiliary streams (after k_runs on s) and join them back
@@ -2250,12 +2340,12 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
     using L192 = BigLayout<D, 192, true>;
     using L128 = BigLayout<D, 128, true>;
     constexpr size_t small_lds = 4 * 64 * (D + 4) * sizeof(float);
-    constexpr size_t lds = std::max({L896::bytes, L384::bytes, L192::bytes, L128::bytes, small_lds});
+    const size_t lds = std::max({L896::bytes, L384::bytes, L192::bytes, L128::bytes, small_lds,
+                                 huge_lds(D, r.dp, 256)});
     static const bool lds_ok =
         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_tail<D>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
     (void)lds_ok;
-    launch_huge(w, slots, dc, r, ctr, n, s);
     const uint32_t nbig = 64, nsmall = 256;
     k_merge_tail<D><<<nbig + nsmall, 256, lds, s>>>(w, slots, dc, r, ctr, nbig);
     return;
@@ -2275,6 +2365,8 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   launch_big<D, 192, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(1));
   launch_big<D, 128, 128, true>(w, 0, slots, dc, r, ctr, n, f.lane(1));
   // every small-run class in one persistent launch (the kernel strides over its batches)
+  // HIP events on its own stream too (bench.py's headline cross-check: this launch is alone on
+  // aux 2, so the event pair measures it, unlike the big-run classes that wait for CU resources)
   if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
   // 12288 one-wave workgroups, 6 per resident slot (2048 at 2 waves per SIMD): the batch stride
   // of a persistent wave is long enough that its rows come from all over the lists, and waves
@@ -2298,7 +2390,7 @@ static void launch_big_wide(const MergeWork& w, int c, uint32_t* slots, const De
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
   const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
   k_merge_big_wide<RB, NT, KC><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist,
-                                                      w.rc);
+                                                      w.rc, w.kt);
 }
 
 static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc,
@@ -2314,13 +2406,19 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
   launch_big_wide<896, 256, 16>(w, 3, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, f.lane(1));
+  // the small-run classes, largest runs first, as one chain on aux 2 (each class fills the chip
+  // with up to 8192 workgroups; a chain on one stream costs only its kernel boundaries)
   RunCounters* rc = w.rc;
-  k_merge_group_wide<64><<<grid(5, 1), 64, 0, f.lane(1)>>>(w.cls[5], 5, slots, dc, r, ctr, w.dlist, rc);
-  k_merge_group_wide<32><<<grid(4, 2), 64, 0, f.lane(1)>>>(w.cls[4], 4, slots, dc, r, ctr, w.dlist, rc);
-  k_merge_group_wide<16><<<grid(3, 4), 64, 0, f.lane(2)>>>(w.cls[3], 3, slots, dc, r, ctr, w.dlist, rc);
-  k_merge_group_wide<8><<<grid(2, 8), 64, 0, f.lane(2)>>>(w.cls[2], 2, slots, dc, r, ctr, w.dlist, rc);
-  k_merge_group_wide<4><<<grid(1, 16), 64, 0, f.lane(2)>>>(w.cls[1], 1, slots, dc, r, ctr, w.dlist, rc);
-  k_merge_group_wide<2><<<grid(0, 32), 64, 0, f.lane(2)>>>(w.cls[0], 0, slots, dc, r, ctr, w.dlist, rc);
+  const hipStream_t sl = f.lane(2);
+  auto group = [&](auto kern, int c, uint32_t per_wave) {
+    kern<<<grid(c, per_wave), 64, 0, sl>>>(w.cls[c], c, slots, dc, r, ctr, w.dlist, rc, w.kt);
+  };
+  group(k_merge_group_wide<64>, 5, 1);
+  group(k_merge_group_wide<32>, 4, 2);
+  group(k_merge_group_wide<16>, 3, 4);
+  group(k_merge_group_wide<8>, 2, 8);
+  group(k_merge_group_wide<4>, 1, 16);
+  group(k_merge_group_wide<2>, 0, 32);
 }
 
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
@@ -2333,9 +2431,12 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   uint32_t* tail_ends = counts + (size_t)kRunRows * ntiles;
   // 8-byte aligned: counts + tail ends take (kRunRows + 1) * ntiles words, rounded up to even
   uint64_t* hbits = reinterpret_cast<uint64_t*>(counts + (((kRunRows + 1u) * ntiles + 1u) & ~1u));
-  k_runs_count<<<ntiles, 256, 0, s>>>(key, lo, n, bucket_thr, ntiles, hbits, tail_ends, counts);
-  k_runs_scan<<<kRunRows, 256, 0, s>>>(counts, ntiles, w.rc);
-  k_runs_write<<<ntiles, 256, 0, s>>>(lo, bucket_thr, ntiles, hbits, tail_ends, counts, w);
+  k_runs_count<<<ntiles, 256, 0, s>>>(key, lo, n, bucket_thr, ntiles, hbits, tail_ends, counts,
+                                      w.kt);
+  const bool fused = ntiles <= 256u;  // the write kernel scans the counts itself
+  if (!fused) k_runs_scan<<<kRunRows, 256, 0, s>>>(counts, ntiles, w.rc);
+  if (fused) k_runs_write<true><<<ntiles, 256, 0, s>>>(lo, bucket_thr, ntiles, hbits, tail_ends, counts, w);
+  else k_runs_write<false><<<ntiles, 256, 0, s>>>(lo, bucket_thr, ntiles, hbits, tail_ends, counts, w);
   switch (r.d) {
     case 8: launch_groups<8>(r, slots, dc, w, ctr, n, s); break;
     case 16: launch_groups<16>(r, slots, dc, w, ctr, n, s); break;

@@ -29,9 +29,10 @@ constexpr int kSortItems = 16;
 template <int B>
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys, uint32_t n,
                                                    int shift, uint32_t ntiles,
-                                                   uint32_t* __restrict__ hist) {
+                                                   uint32_t* __restrict__ hist, KTime kt) {
   constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u;
   __shared__ uint32_t c[RAD];
+  kt_begin(kt, KC_SORT);  // (only the first pass's launch carries kt)
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   for (uint32_t d = t; d < RAD; d += 256) c[d] = 0u;
   const uint32_t base = blockIdx.x * kSortTile + wv * 1024u + lane;
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
                                                       uint32_t* __restrict__ vout, uint32_t n,
                                                       int shift, uint32_t ntiles,
                                                       const uint32_t* __restrict__ hist,
-                                                      const uint32_t* __restrict__ dtot) {
+                                                      const uint32_t* __restrict__ dtot, KTime kt) {
   constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u, PER = RAD / 256u;
   __shared__ uint32_t lk[kSortTile], lv[kSortTile];
   __shared__ uint32_t wc[4][RAD];  // per-wave running digit counts, then their wave prefixes
@@ -159,6 +160,7 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
     kout[o] = kk;
     vout[o] = lv[e];
   }
+  kt_end(kt, KC_SORT);  // (only the last pass's launch carries kt)
 }
 
 uint64_t sort_ws_words(uint64_t slots) {
@@ -166,19 +168,22 @@ uint64_t sort_ws_words(uint64_t slots) {
   return 1024ull * ((slots + kSortTile - 1) / kSortTile) + 1024 + 64;
 }
 
+// first / last: the pass opens / closes the sort's timed span (kt may be null)
 template <int B>
 static void sort_pass(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo,
-                      uint32_t n, int shift, uint32_t* ws, hipStream_t s) {
+                      uint32_t n, int shift, uint32_t* ws, hipStream_t s, KTime kt,
+                      bool first, bool last) {
   const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
   uint32_t* hist = ws;
   uint32_t* dtot = ws + (size_t)(1u << B) * ntiles;
-  k_sort_hist<B><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, hist);
+  k_sort_hist<B><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, hist, first ? kt : kNoTime);
   k_sort_dscan<<<1u << B, 256, 0, s>>>(hist, ntiles, dtot);
-  k_sort_scatter<B><<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, hist, dtot);
+  k_sort_scatter<B><<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, hist, dtot,
+                                           last ? kt : kNoTime);
 }
 
 void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
-                uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s) {
+                uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s, KTime kt) {
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
   if (n > 1 && bits > 0) {
     // P passes of B-bit digits: 1..10 bits one pass, 11..20 two, 21..30 three, 31..32 four
@@ -186,9 +191,10 @@ void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t
     const int B = std::max(8, (bits + P - 1) / P);
     for (int p = 0; p < P; ++p) {
       const int shift = p * B;
-      if (B == 8) sort_pass<8>(ki, vi, ko, vo, n, shift, ws, s);
-      else if (B == 9) sort_pass<9>(ki, vi, ko, vo, n, shift, ws, s);
-      else sort_pass<10>(ki, vi, ko, vo, n, shift, ws, s);
+      const bool first = p == 0, last = p == P - 1;
+      if (B == 8) sort_pass<8>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last);
+      else if (B == 9) sort_pass<9>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last);
+      else sort_pass<10>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last);
       std::swap(ki, ko);
       std::swap(vi, vo);
     }

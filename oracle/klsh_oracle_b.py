@@ -12,9 +12,16 @@ Restated from (paths under /root/reference):
                   65535, coverage = float sum of log(count) in file order.  A database listing
                   fewer k-mers than its total adds the all-A k-mer (the default-constructed Kmer
                   left in KmcRead's vector).
-The reference's row order is libcuckoo's table order; rows here are in first-appearance order
-(sample order, then file order), the order the product writes.  Pinned by tests/golden/mode_b.json
-(the reference's own outputs, compared as rows keyed by k-mer).
+  cuckoo_order    the row order: the reference's libcuckoo table (hash/HashTables.h:22, the
+                  vendored utils/libcuckoo/cuckoohash_map.hh: 8-slot buckets, 2^16 of them to start,
+                  index_hash / alt_index :893-908, cuckoo_insert :1428-1483, BFS slot_search
+                  :983-1022, cuckoopath_move :1124-1176, cuckoo_expand_simple :1627-1667) after
+                  KmcRead's inserts at -T 1 (kmer/kmc_reader.cc:5-20, 66-70) — a duplicate insert
+                  changes nothing, so it is the distinct k-mers inserted in first-appearance order —
+                  iterated bucket by bucket, slot by slot (io/ioHT.cc:140-149).  Kmer::hash()
+                  (kmer/Kmer.cc:138-147) is hash/hash.cc's early MurmurHash3_x64_128 revision.
+Pinned by tests/golden/mode_b.json: the reference CLI's own kmer_set.hex / kmer_count.bin md5s
+(byte for byte) on the small cases and on a table loaded to 95.6 % (long cuckoo paths).
 """
 from __future__ import annotations
 
@@ -41,19 +48,21 @@ def read_kmc(name: str):
         total = struct.unpack_from("<Q", pre, h + 28)[0]
         sig_size = (1 << (2 * sig_len)) + 1
         lut_bytes = size - (sig_size * 4 + header_offset + 8)
-        lut = list(struct.unpack_from("<%dQ" % ((lut_bytes + 8) // 8), pre, 4))
+        lut = np.frombuffer(pre, "<u8", (lut_bytes + 8) // 8, 4).astype(np.uint64)
         lut[lut_bytes // 8] = total + 1
+        lut = lut[:lut_bytes // 8 + 1]
     elif version == 0:
         n = (size - 4) // 8
-        buf = list(struct.unpack_from("<%dQ" % n, pre, 4))
+        buf = np.frombuffer(pre, "<u8", n, 4).astype(np.uint64)
         size -= 4
         hi = (size - header_offset) // 8
-        k, mode = buf[hi] & 0xFFFFFFFF, buf[hi] >> 32
-        counter_size, p = buf[hi + 1] & 0xFFFFFFFF, buf[hi + 1] >> 32
-        min_count, max_count = buf[hi + 2] & 0xFFFFFFFF, buf[hi + 2] >> 32
-        total = buf[hi + 3]
-        max_count += buf[hi + 4] & 0xFFFFFFFF00000000
-        lut = buf
+        w = [int(x) for x in buf[hi:hi + 5]]
+        k, mode = w[0] & 0xFFFFFFFF, w[0] >> 32
+        counter_size, p = w[1] & 0xFFFFFFFF, w[1] >> 32
+        min_count, max_count = w[2] & 0xFFFFFFFF, w[2] >> 32
+        total = w[3]
+        max_count += w[4] & 0xFFFFFFFF00000000
+        lut = buf[:hi + 1].copy()
         lut[hi] = total + 1
     else:
         raise ValueError("KMC version %#x" % version)
@@ -61,20 +70,20 @@ def read_kmc(name: str):
     sufix_size = (k - p) // 4
     rec = sufix_size + counter_size
     mask = (1 << (2 * p)) - 1
-    out = []
-    pi = 0
     data = suf[4:-4]
     assert len(data) == total * rec, (len(data), total, rec)
-    for r in range(total):
-        if r == lut[pi + 1]:
-            pi += 1
-            while lut[pi] == lut[pi + 1]:
-                pi += 1
-        o = r * rec
-        sv = int.from_bytes(data[o:o + sufix_size], "big") if sufix_size else 0
-        cnt = int.from_bytes(data[o + sufix_size:o + rec], "little")
-        if min_count <= cnt <= max_count:
-            out.append((((pi & mask) << (2 * (k - p))) | sv, cnt))
+    # record r's prefix: the reader's LUT walk (skipping empty prefixes) = the last LUT entry <= r
+    pis = np.searchsorted(lut, np.arange(total, dtype=np.uint64), side="right") - 1
+    recs = np.frombuffer(data, np.uint8).reshape(total, rec) if total else np.zeros((0, rec), np.uint8)
+    sv = np.zeros(total, np.uint64)
+    for b in range(sufix_size):  # big-endian suffix
+        sv = (sv << np.uint64(8)) | recs[:, b].astype(np.uint64)
+    cnt = np.zeros(total, np.uint64)
+    for b in range(counter_size):  # little-endian counter
+        cnt |= recs[:, sufix_size + b].astype(np.uint64) << np.uint64(8 * b)
+    vals = ((pis.astype(np.uint64) & np.uint64(mask)) << np.uint64(2 * (k - p))) | sv
+    keep = (cnt >= np.uint64(min_count)) & (cnt <= np.uint64(max_count))
+    out = list(zip(vals[keep].tolist(), cnt[keep].tolist()))
     return k, out, total
 
 
@@ -93,8 +102,126 @@ def canonical(img: int, k: int) -> int:
     return img if img.to_bytes(8, "little") < t.to_bytes(8, "little") else t
 
 
-def build_khtable(names, k: int):
-    """(reps in first-appearance order, counts [d][kmap] uint16, log text)."""
+M64 = (1 << 64) - 1
+
+
+def kmer_hash(img: int, k: int) -> int:
+    """Kmer::hash(): the first word of hash/hash.cc's MurmurHash3_x64_128 (seed 0) over the
+    Kmer's (k+3)/4 bytes — one tail block (k1 = those bytes little-endian, k2 = 0)."""
+    nb = (k + 3) // 4
+
+    def rotl(v, r):
+        return ((v << r) | (v >> (64 - r))) & M64
+
+    def fmix(x):
+        x ^= x >> 33
+        x = (x * 0xff51afd7ed558ccd) & M64
+        x ^= x >> 33
+        x = (x * 0xc4ceb9fe1a85ec53) & M64
+        return x ^ (x >> 33)
+
+    h1, h2 = 0x9368e53c2f6af274, 0x586dcd208f7cd3fd
+    c1, c2 = 0x87c37b91114253d5, 0x4cf5ad432745937f
+    k1 = img & ((1 << (8 * nb)) - 1)
+    k1 = (rotl((k1 * c1) & M64, 23) * c2) & M64       # bmix64 (hash.cc:73-92), k2 = 0
+    h1 = ((h1 ^ k1) + h2) & M64
+    h2 = (rotl(h2, 41) + h1) & M64
+    h1 = (h1 * 3 + 0x52dce729) & M64
+    h2 = (h2 * 3 + 0x38495ab5) & M64
+    h2 ^= nb                                            # finalization (hash.cc:160-172)
+    h1 = (h1 + h2) & M64
+    h2 = (h2 + h1) & M64
+    return (fmix(h1) + fmix(h2)) & M64
+
+
+def cuckoo_order(reps, k: int, hashpower: int = 16):
+    """Indices of `reps` (distinct, in insertion order) in the table's iteration order, and the
+    final hash power."""
+    SLOTS, MAXD, QN = 8, 4, 501
+    hv = [kmer_hash(int(r), k) for r in reps]
+    st = {"hp": hashpower}
+    tab = [-1] * (SLOTS << hashpower)
+
+    def alt(h, b):
+        m = (1 << st["hp"]) - 1
+        return (b ^ ((((h >> st["hp"]) + 1) * 0x5bd1e995) & M64)) & m
+
+    def free_slot(b):
+        for s in range(SLOTS):
+            if tab[b * SLOTS + s] < 0:
+                return s
+        return -1
+
+    def search(a, b):  # slot_search: (bucket, pathcode, depth) or None
+        q = [None] * QN
+        first, last = 0, 0
+        nxt = lambda i: 0 if i == QN - 1 else i + 1  # noqa: E731
+        q[last] = (a, 0, 0); last = nxt(last)          # noqa: E702
+        q[last] = (b, 1, 0); last = nxt(last)          # noqa: E702
+        while nxt(last) != first:
+            xb, xp, xd = q[first]
+            first = nxt(first)
+            s = 0
+            while s < SLOTS and nxt(last) != first:
+                e = tab[xb * SLOTS + s]
+                if e < 0:
+                    return xb, xp * SLOTS + s, xd
+                yb = alt(hv[e], xb)
+                yp, yd = xp * SLOTS + s, xd + 1
+                j = free_slot(yb)
+                if j >= 0:
+                    return yb, yp * SLOTS + j, yd
+                if yd != MAXD:
+                    q[last] = (yb, yp, yd)
+                    last = nxt(last)
+                s += 1
+        return None
+
+    def insert(e):
+        while True:
+            m = (1 << st["hp"]) - 1
+            a = hv[e] & m
+            b = alt(hv[e], a)
+            for bk in (a, b):
+                s = free_slot(bk)
+                if s >= 0:
+                    tab[bk * SLOTS + s] = e
+                    return
+            found = search(a, b)
+            if found is None:
+                expand()
+                continue
+            _, code, depth = found
+            slots = [0] * (depth + 1)
+            for i in range(depth, -1, -1):
+                slots[i] = code % SLOTS
+                code //= SLOTS
+            buckets = [a if code == 0 else b]
+            for i in range(1, depth + 1):
+                pe = tab[buckets[i - 1] * SLOTS + slots[i - 1]]
+                buckets.append(alt(hv[pe], buckets[i - 1]))
+            for dd in range(depth, 0, -1):
+                tab[buckets[dd] * SLOTS + slots[dd]] = tab[buckets[dd - 1] * SLOTS + slots[dd - 1]]
+                tab[buckets[dd - 1] * SLOTS + slots[dd - 1]] = -1
+            tab[buckets[0] * SLOTS + slots[0]] = e
+            return
+
+    def expand():
+        old = [v for v in tab if v >= 0]
+        st["hp"] += 1
+        tab[:] = [-1] * (SLOTS << st["hp"])
+        for v in old:
+            insert(v)
+
+    for e in range(len(reps)):
+        insert(e)
+    return [v for v in tab if v >= 0], st["hp"]
+
+
+def build_khtable(names, k: int, order: str = "reference"):
+    """(reps, counts [d][kmap] uint16, log text); rows in the reference's libcuckoo order, or in
+    first-appearance order (order="first")."""
+    order_kind = order
     order, index = [], {}
     listed = []
     for nm in names:
@@ -119,6 +246,10 @@ def build_khtable(names, k: int):
             cov = np.float32(np.float64(cov) + math.log(c))
         counts[j] = acc.astype(np.uint16)
         log += "\t%f" % float(cov)
+    if order_kind == "reference":
+        idx, _ = cuckoo_order(order, k)
+        order = [order[i] for i in idx]
+        counts = counts[:, idx]
     return order, counts, log
 
 

@@ -126,7 +126,13 @@ int main(int argc, char** argv) {
   fclose(bf);
 
   klsh_oracle_rng rng = {seed, 0};
-  const uint64_t batch_thresh = 100000000ull;
+  /* app/kmerLSH.cc's 1e8-row batch size; KLSH_TEST_BATCH_THRESH (>= 1000) overrides it for the
+   * tests of the multi-batch init and re-cluster branch */
+  uint64_t batch_thresh = 100000000ull;
+  {
+    const char* e = getenv("KLSH_TEST_BATCH_THRESH");
+    if (e && strtoull(e, NULL, 10) >= 1000) batch_thresh = strtoull(e, NULL, 10);
+  }
   rowset cur = {0}, next = {0};
   /* init_clustering first pass (app/kmerLSH.cc:303-345): batches of 1e8 rows, I=1, bthr 1e5. */
   float similarity = min_sim;
@@ -187,5 +193,8 @@ int main(int argc, char** argv) {
   fclose(fc);
   fclose(fb);
   printf("clusters: %llu\n", (unsigned long long)fin.n);
+  free(v_kmers);
+  free(cur.rows); free(cur.off); free(cur.ids);
+  free(fin.rows); free(fin.off); free(fin.ids);
   return 0;
 }

@@ -51,29 +51,29 @@ def write_db(path: str, k: int, records, version: int, p: int, counter_size: int
         v = kmer_value(s)
         b = (v * 0x9E3779B97F4A7C15 >> 61) % nb if nb > 1 else 0
         per_bin[b].append((v >> (2 * suf_sym), v & ((1 << (2 * suf_sym)) - 1), c))
+    import numpy as np
+
     L = 1 << (2 * p)
-    lut = []
+    luts = []
     recs = bytearray()
     total = 0
     for b in range(nb):
         rs = sorted(per_bin[b])
-        counts_per_prefix = [0] * L
-        for pre, _, _ in rs:
-            counts_per_prefix[pre] += 1
-        acc = total
-        for i in range(L):
-            lut.append(acc)
-            acc += counts_per_prefix[i]
+        counts_per_prefix = np.bincount(np.array([pre for pre, _, _ in rs], np.int64),
+                                        minlength=L).astype(np.uint64)
+        # lut[i] = total + records with a smaller prefix (an exclusive running sum)
+        luts.append(np.uint64(total) + np.concatenate([[0], np.cumsum(counts_per_prefix)[:-1]]).astype(np.uint64))
         for pre, suf, c in rs:
             recs += suf.to_bytes(sufix_size, "big") if sufix_size else b""
             recs += int(c).to_bytes(counter_size, "little")
         total += len(rs)
+    lut = np.concatenate(luts).astype("<u8")
     with open(path + ".kmc_suf", "wb") as f:
         f.write(b"KMCS" + bytes(recs) + b"KMCS")
     both = 0  # stored flag 0 = "both strands" (the reader negates it)
     with open(path + ".kmc_pre", "wb") as f:
         f.write(b"KMCP")
-        f.write(struct.pack("<%dQ" % len(lut), *lut))
+        f.write(lut.tobytes())
         if version == 0:
             hdr = struct.pack("<5Q", k | (0 << 32), counter_size | (p << 32),
                               min_count | ((max_count & 0xFFFFFFFF) << 32), total, both)
@@ -130,3 +130,73 @@ def write_case(dirpath: str, case: str) -> dict:
 def cli_args(case: str) -> list:
     return ["-a", "a.txt", "-b", "b.txt", "-o", "A", "-p", "B", "-K", str(CASES[case]["k"]), "-M", "B",
             "--only", "--verbose", "-T", "1"]
+
+
+# Large mode-B cases (the reference's libcuckoo table under load): KMC1 databases of random
+# k-mers drawn from a vectorised splitmix64 stream, written with numpy (the per-record writer above
+# is too slow for 10^5..10^6 records).  "bl_fill": ~470K distinct k-mers, one table of 2^16 8-slot
+# buckets at ~90 % load (long cuckoo paths); "bl_grow": ~640K, past what that table holds, so it
+# doubles once.
+BIG_CASES = {
+    "bl_fill": dict(k=31, p=11, samples=2, per_sample=276_000, overlap=0.43, seed=101),
+    "bl_grow": dict(k=31, p=11, samples=2, per_sample=400_000, overlap=0.40, seed=103),
+}
+
+
+def _splitmix_np(seed: int, n: int):
+    import numpy as np
+
+    x = (np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) + np.uint64(seed)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def write_big_case(dirpath: str, case: str) -> dict:
+    """Sample j lists per_sample k-mers: an `overlap` share drawn from a pool common to all
+    samples, the rest its own; counts 1..200 (1-byte counters), KMC1 layout, sorted records."""
+    import numpy as np
+
+    c = BIG_CASES[case]
+    k, p, n = c["k"], c["p"], c["per_sample"]
+    kmask = np.uint64((1 << (2 * k)) - 1)
+    shared = _splitmix_np(c["seed"], n) & kmask
+    names = []
+    for j in range(c["samples"]):
+        own = _splitmix_np(c["seed"] * 7919 + j + 1, n) & kmask
+        pick = _splitmix_np(c["seed"] * 104729 + j, n) % np.uint64(1000) < np.uint64(int(c["overlap"] * 1000))
+        vals = np.unique(np.where(pick, shared, own))
+        cnt = (_splitmix_np(c["seed"] + 17 * j, vals.size) % np.uint64(200) + np.uint64(1)).astype(np.uint8)
+        suf_sym = k - p
+        pre = (vals >> np.uint64(2 * suf_sym)).astype(np.int64)
+        suf = vals & np.uint64((1 << (2 * suf_sym)) - 1)
+        sb = suf_sym // 4
+        rec = np.zeros((vals.size, sb + 1), np.uint8)
+        for b in range(sb):  # big-endian suffix bytes
+            rec[:, b] = ((suf >> np.uint64(8 * (sb - 1 - b))) & np.uint64(0xFF)).astype(np.uint8)
+        rec[:, sb] = cnt
+        lut = np.zeros(1 << (2 * p), np.uint64)
+        np.add.at(lut, pre, 1)
+        lut = np.concatenate([[0], np.cumsum(lut)[:-1]]).astype("<u8")
+        name = "db%d" % j
+        path = os.path.join(dirpath, name)
+        with open(path + ".kmc_suf", "wb") as f:
+            f.write(b"KMCS" + rec.tobytes() + b"KMCS")
+        with open(path + ".kmc_pre", "wb") as f:
+            f.write(b"KMCP")
+            f.write(lut.tobytes())
+            hdr = struct.pack("<5Q", k, 1 | (p << 32), 1 | (255 << 32), vals.size, 0)
+            f.write(hdr)
+            f.write(struct.pack("<I", len(hdr)))
+            f.write(b"KMCP")
+        names.append(name)
+    with open(os.path.join(dirpath, "a.txt"), "w") as f:
+        f.write("s0.fq %s\n" % names[0])
+    with open(os.path.join(dirpath, "b.txt"), "w") as f:
+        f.write("".join("s%d.fq %s\n" % (j, names[j]) for j in range(1, c["samples"])))
+    return dict(c, d=c["samples"], names=names)
+
+
+def big_cli_args(case: str) -> list:
+    return ["-a", "a.txt", "-b", "b.txt", "-o", "A", "-p", "B", "-K", str(BIG_CASES[case]["k"]),
+            "-M", "B", "--only", "--verbose", "-T", "1"]

@@ -335,6 +335,32 @@ def test_cli_kat_md5(kat, tmp_path):
     assert trace == ref["trace"]
 
 
+@pytest.mark.parametrize("thresh", [3000, 7000])
+def test_cli_recluster_branch_vs_oracle(oracle, thresh, tmp_path):
+    """init_clustering's multi-batch first pass and its `while (total > batch_thresh)` re-cluster
+    passes (similarity -= 0.001, I + 4; app/kmerLSH.cc:303-411), reached on katF's 20K rows by the
+    test-only KLSH_TEST_BATCH_THRESH override in both CLIs: the product's outputs equal the oracle
+    CLI's byte for byte.  (Pinned product <-> oracle only: the reference hard-codes 1e8, and
+    reaching the branch there needs > 1e8 k-mers.)"""
+    import kat_inputs
+    from kmerlsh_amd import _native
+
+    outs = {}
+    for name, cli in (("gpu", _native.CLI_PATH), ("oracle", oracle.CLI)):
+        d = tmp_path / name
+        kat_inputs.write_kat("katF", str(d))
+        env = dict(os.environ, KLSH_TEST_BATCH_THRESH=str(thresh))
+        out = subprocess.run([cli, "-a", "a.txt", "-b", "b.txt", "-I", "10", "-T", "2", "-M", "C",
+                              "--only", "--seed", "12345", "--verbose"], cwd=d, check=True,
+                             capture_output=True, text=True, timeout=300, env=env).stdout
+        trace = [int(line.split(":")[1]) for line in out.splitlines() if line.startswith("Size of")]
+        outs[name] = (trace, {fn: hashlib.md5(open(d / fn, "rb").read()).hexdigest()
+                              for fn in ("clustering_result.txt", "clustering_result.txt.clust")})
+    assert outs["gpu"] == outs["oracle"]
+    # the branch ran: more than one init batch and at least one re-cluster pass
+    assert len(outs["gpu"][0]) > 10 + 20000 // thresh
+
+
 def test_synth_mode_c_vs_oracle(engine, oracle):
     """klsh-synth counts -> GPU convert -> init pass -> main loop, against the oracle."""
     from kmerlsh_amd import _native

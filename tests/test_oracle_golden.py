@@ -137,3 +137,23 @@ def test_kat_end_to_end(oracle, kat, tmp_path):
             assert hashlib.md5(f.read()).hexdigest() == md5, fn
     trace = [int(line.split(":")[1]) for line in out.splitlines() if line.startswith("Size of")]
     assert trace == ref["trace"]
+
+
+def test_oracle_cli_recluster_branch(oracle, tmp_path):
+    """The oracle CLI's multi-batch init and re-cluster passes (app/kmerLSH.cc:303-411) through the
+    test-only KLSH_TEST_BATCH_THRESH override: every pass appears in the trace, the survivors shrink
+    below the threshold before the main loop, and the run is deterministic."""
+    kat_inputs.write_kat("katF", str(tmp_path))
+    env = dict(os.environ, KLSH_TEST_BATCH_THRESH="3000")
+    runs = []
+    for _ in range(2):
+        out = subprocess.run([oracle.CLI, "-a", "a.txt", "-b", "b.txt", "-I", "10", "-T", "2",
+                              "-M", "C", "--only", "--seed", "12345", "--verbose"], cwd=tmp_path,
+                             check=True, capture_output=True, text=True, env=env).stdout
+        trace = [int(line.split(":")[1]) for line in out.splitlines() if line.startswith("Size of")]
+        with open(tmp_path / "clustering_result.txt", "rb") as f:
+            runs.append((trace, hashlib.md5(f.read()).hexdigest()))
+    assert runs[0] == runs[1]
+    trace = runs[0][0]
+    assert len(trace) > 10 + 20000 // 3000  # init batches + re-cluster passes + the main loop
+    assert trace[-10] <= 3000  # the main loop starts below the batch threshold
