@@ -289,7 +289,7 @@ KERNEL_NAMES = {
     "big128": "k_merge_big<{d},128,128,true>", "big192": "k_merge_big<{d},192,256,true>",
     "big384": "k_merge_big<{d},384,256,true>", "big896": "k_merge_big<{d},896,256,false>",
     "huge": "k_merge_huge<{d}>", "tail": "k_merge_tail<{d}>",
-    "compact": "k_compact_count/apply (span)",
+    "compact": "k_compact_count/apply (span)", "pairs": "k_merge_pairs<{d}>",
 }
 WIDE_NAMES = {
     "project": "k_project_mfma_wide + k_project_fix (span)",

@@ -39,9 +39,10 @@ extern "C" {
 
 typedef struct klsh_ctx klsh_ctx;
 
-/* Per-kernel-class statistics of a call: HIP-event time of the class's launches (events bound to
- * the dispatches themselves), launches, and the rows they handled (the unit of each class's
- * algorithmic bytes).  Index = KLSH_K_*. */
+/* Per-kernel-class statistics of a call: summed span of the class's launches (first workgroup
+ * start to last workgroup end, read from the GPU clock inside the kernels), launches, and the
+ * rows they handled (the unit of each class's algorithmic bytes).
+ * Index = KLSH_K_*. */
 #define KLSH_K_PROJECT 0  /* sign-hash of every live row (k_project_*) */
 #define KLSH_K_SORT 1     /* stable bucket sort, all passes (span of the first to last launch) */
 #define KLSH_K_RUNS 2     /* run finding and size-class lists (span) */
@@ -53,6 +54,7 @@ typedef struct klsh_ctx klsh_ctx;
 #define KLSH_K_HUGE 8     /* longer runs (k_merge_huge) */
 #define KLSH_K_TAIL 9     /* iterations below 2^20 positions: every merge class in one k_merge_tail */
 #define KLSH_K_COMPACT 10 /* survivor compaction (span) */
+#define KLSH_K_PAIRS 11   /* runs of 2 rows when they have a launch of their own (else in SMALL) */
 #define KLSH_KCLASSES 12
 typedef struct klsh_kstat {
   double ms;

@@ -566,8 +566,20 @@ klsh_ctx* klsh_create(int device, int* err) {
   const bool big_prio = true;
   bool ok = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking,
                                         big_prio ? prio_hi : prio_lo) == hipSuccess;
-  for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
-  for (auto& e : c->sev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  // Every event here only times work or orders streams of this device: none makes device
+  // writes visible to the host (the counters come back through the published mapped line, with
+  // its own system-scope release).  A default event ends with a system-scope release — an L2
+  // writeback of everything the kernel before it wrote, 6-16 us of stream time per event on C2
+  // (the projection -> sort and fork / join gaps of the round-3 trace) — so timing events skip
+  // the fence and the fork / join events release at device scope (KLSH_EVENT_FENCE=1: defaults).
+  static const bool fence = [] {
+    const char* e = getenv("KLSH_EVENT_FENCE");
+    return e && atoi(e) != 0;
+  }();
+  const unsigned tflags = fence ? hipEventDefault : hipEventDisableSystemFence;
+  const unsigned oflags = hipEventDisableTiming | (fence ? 0u : hipEventReleaseToDevice);
+  for (auto& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, tflags) == hipSuccess;
+  for (auto& e : c->sev) ok = ok && hipEventCreateWithFlags(&e, tflags) == hipSuccess;
   for (int i = 0; i < klsh::kMergeStreams; ++i) {
 #ifdef KLSH_AUX1_HI  // A/B: the 65..192-row stream at the high priority too
     const bool hi = i <= 1;
@@ -576,9 +588,9 @@ klsh_ctx* klsh_create(int device, int* err) {
 #endif
     ok = ok && hipStreamCreateWithPriority(&c->mw.aux[i], hipStreamNonBlocking,
                                            (hi && big_prio) ? prio_hi : prio_lo) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&c->mw.join[i], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&c->mw.join[i], oflags) == hipSuccess;
   }
-  ok = ok && hipEventCreateWithFlags(&c->mw.fork, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->mw.fork, oflags) == hipSuccess;
   ok = ok && hipMalloc((void**)&c->ctr, sizeof(Counters)) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) == hipSuccess;
   ok = ok && hipMemset(c->ctr, 0, sizeof(Counters)) == hipSuccess;  // err starts clear

@@ -84,7 +84,7 @@ struct Counters {
 // order) and clears it; the engine folds the last set at the end of a call.
 enum KClass : int {
   KC_PROJECT = 0, KC_SORT, KC_RUNS, KC_SMALL, KC_BIG128, KC_BIG192, KC_BIG384, KC_BIG896, KC_HUGE,
-  KC_TAIL, KC_COMPACT, KC_COUNT
+  KC_TAIL, KC_COMPACT, KC_PAIRS, KC_COUNT
 };
 constexpr int kStampSlots = 16;
 struct alignas(128) StampLine {

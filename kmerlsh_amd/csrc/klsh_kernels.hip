@@ -88,7 +88,11 @@ __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X,
 #pragma unroll
   for (int r = 0; r < RPL; ++r) {
     const uint32_t pr = p0 + 256u * r;
+#ifdef KLSH_PROJ_IDENT  // diagnostics build only: rows in position order (wrong keys)
+    const float4* src = reinterpret_cast<const float4*>(X + (size_t)(pr < n ? pr : p0) * dp);
+#else
     const float4* src = reinterpret_cast<const float4*>(X + (size_t)slots[pr < n ? pr : p0] * dp);
+#endif
 #pragma unroll
     for (int m = 0; m < D / 4; ++m) {
       const float4 v = src[m];
@@ -132,9 +136,20 @@ __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X,
                  (a[r][c][0].y >= 0.0f ? 4u : 0u) + (a[r][c][1].x >= 0.0f ? 2u : 0u) +
                  (a[r][c][1].y >= 0.0f ? 1u : 0u);
   };
+#ifdef KLSH_PROJ_NOVALU  // diagnostics build only: the row loads without the chains (wrong keys)
+  (void)quads;
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    float sacc = 0.0f;
+#pragma unroll
+    for (int m = 0; m < D / 2; ++m) sacc += x[r][m].x + x[r][m].y;
+    key[r] = (__float_as_uint(sacc) * 2654435761u) >> (32 - 4 * nq);
+  }
+#else
   int q = 0;
   for (; q + CH <= nq; q += CH) quads(q, std::integral_constant<int, CH>{});
   for (; q < nq; ++q) quads(q, std::integral_constant<int, 1>{});
+#endif
 #pragma unroll
   for (int r = 0; r < RPL; ++r) {
     const uint32_t pr = p0 + 256u * r;

@@ -24,6 +24,7 @@
 // Results are positional (survivors in place, kInvalid after), so they do not depend on which
 // wave handled which run or in what order.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -194,10 +195,14 @@ __device__ __forceinline__ uint32_t prescreen(const Decider& dc, float g, float 
 //    state to lane i (swap-remove), remaps bit `last` to bit i everywhere, and re-decides bit j
 //    for the positions still to be visited — through the certified short-chain screen, exact
 //    chains only for close calls — whose ballot is the new row's P.
-template <int G, int D>
+// GT: the group width at compile time, or 0: g_rt at run time (one code path for every class:
+// the persistent small-run loop then needs the registers of one instance, not of five).
+template <int GT, int D>
 __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slot,
                                             uint32_t* slots, const Decider& dc, const Rows& r,
-                                            float* lds, uint32_t* dlist, Counters* ctr) {
+                                            float* lds, uint32_t* dlist, Counters* ctr,
+                                            uint32_t g_rt = 0) {
+  const uint32_t G = GT ? (uint32_t)GT : g_rt;
   constexpr int ST = D + 4;  // padded row stride: 16 lanes of a ds_read_b128 hit distinct banks
   const uint32_t lane = __lane_id();
   const uint32_t g = lane & (G - 1);
@@ -410,7 +415,7 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
 #ifdef KLSH_MERGE_PROF
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (lane == 0) {
-    constexpr int c = G == 4 ? 1 : G == 8 ? 2 : G == 16 ? 3 : G == 32 ? 4 : 5;
+    const int c = (int)__builtin_ctz(G) - 1;
     const uint64_t sp4 = WPROF_CLK();
     atomicAdd(&g_sprof[c][0], 1ull);
     atomicAdd(&g_sprof[c][1], sp1 - sp0);
@@ -486,8 +491,9 @@ __device__ __forceinline__ void pair_batch(const uint2* __restrict__ list, uint3
 }
 
 // One wave's share of the small-run batches: waves `wave`, `wave + nwaves`, ... of the batch
-// space; lds = this wave's 64 * (D + 4) floats.
-template <int D>
+// space; lds = this wave's 64 * (D + 4) floats.  WHICH: 0 = every class, 1 = the pairs only,
+// 2 = runs of 3..64 rows only.
+template <int D, int WHICH = 0>
 __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restrict__ slots,
                                            const Decider& dc, const Rows& r, Counters* ctr,
                                            float* lds, uint32_t wave, uint32_t nwaves) {
@@ -495,7 +501,9 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
   uint32_t n[NC], nb[NC], start[NC + 1];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
-    n[c] = __hip_atomic_load(&w.rc->n_cls[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    n[c] = (WHICH == 1 && c > 0) || (WHICH == 2 && c == 0)
+               ? 0u
+               : __hip_atomic_load(&w.rc->n_cls[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   nb[0] = (n[0] + 63u) / 64u;
   nb[1] = batches_of<4>(n[1]);
   nb[2] = batches_of<8>(n[2]);
@@ -530,7 +538,7 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
     int c;
     uint32_t bi;
     locate(t, c, bi);
-    if (c == 0) return;  // pairs load their own
+    if (WHICH == 1 || c == 0) return;  // pairs load their own
     const uint32_t G = 2u << c, NG = 64u / G;
     const uint32_t k = bi * NG + lane / G, g = lane & (G - 1);
     if (k < n[c]) {
@@ -548,28 +556,54 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
     int c;
     uint32_t bi;
     locate(t, c, bi);
+    if constexpr (WHICH == 1) {
+      pair_batch<D>(w.cls[0], n[0], bi, slots, dc, r, ctr, w.dlist);
+      continue;
+    }
+#ifdef KLSH_SMALL_RT_G
+    if (WHICH != 2 && c == 0) pair_batch<D>(w.cls[0], n[0], bi, slots, dc, r, ctr, w.dlist);
+    else merge_batch<0, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr, 2u << c);
+#else
     switch (c) {  // wave-uniform
-      case 0: pair_batch<D>(w.cls[0], n[0], bi, slots, dc, r, ctr, w.dlist); break;
+      case 0:
+        if constexpr (WHICH != 2) pair_batch<D>(w.cls[0], n[0], bi, slots, dc, r, ctr, w.dlist);
+        break;
       case 1: merge_batch<4, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
       case 2: merge_batch<8, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
       case 3: merge_batch<16, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
       case 4: merge_batch<32, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
       default: merge_batch<64, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
     }
+#endif
     e = e_next;
     slot = slot_next;
   }
 }
 
+#ifdef KLSH_SPLIT_PAIRS
+constexpr int kSmallWhich = 2;  // runs of 3..64 rows here, the pairs in k_merge_pairs
+#else
+constexpr int kSmallWhich = 0;
+#endif
 template <int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_merge_small(
     MergeWork w, uint32_t* __restrict__ slots,
                                                     Decider dc, Rows r, Counters* ctr) {
   __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
   kt_begin(w.kt, KC_SMALL);
-  small_loop<D>(w, slots, dc, r, ctr, lds, blockIdx.x, gridDim.x);
+  small_loop<D, kSmallWhich>(w, slots, dc, r, ctr, lds, blockIdx.x, gridDim.x);
   kt_end(w.kt, KC_SMALL);
 }
+#ifdef KLSH_SPLIT_PAIRS
+// The runs of exactly 2 rows alone: no LDS and fewer registers, so three waves per SIMD.
+template <int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_merge_pairs(
+    MergeWork w, uint32_t* __restrict__ slots, Decider dc, Rows r, Counters* ctr) {
+  kt_begin(w.kt, KC_PAIRS);
+  small_loop<D, 1>(w, slots, dc, r, ctr, nullptr, blockIdx.x, gridDim.x);
+  kt_end(w.kt, KC_PAIRS);
+}
+#endif
 
 // Runs of equal keys, listed by size class, in three launches and no contended atomics:
 //   k_runs_count  a tile of 4096 positions is read coalesced (position k*256 + t by thread t), its
@@ -2373,6 +2407,10 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   // retire and re-enter as the big-run workgroups come and go (C2, same box, interleaved:
   // 4608 -> 255.9 / 258.0 ms, 8192 -> 255.4 / 252.3, 12288 -> 250.8 / 251.7, 16384 -> 256.0 /
   // 253.9; small-run merge 79.4 -> 70.5 ms per step)
+#ifdef KLSH_SPLIT_PAIRS
+  static const int pairs_lane = getenv("KLSH_PAIRS_MAIN") ? 3 : 2;
+  k_merge_pairs<D><<<12288, 64, 0, pairs_lane == 3 ? s : f.lane(2)>>>(w, slots, dc, r, ctr);
+#endif
   k_merge_small<D><<<12288, 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
   if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[1], f.lane(2));
 }
