@@ -23,6 +23,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <deque>
 #include <functional>
 #include <numeric>
 #include <string>
@@ -163,6 +164,11 @@ struct klsh_ctx {
   uint32_t* pub_seq_host = nullptr;
   uint32_t* pub_seq_dev = nullptr;
   uint32_t pub_seq = 0;
+  // Queued tail batches (run_batched): every iteration publishes into its own ring slot, the host
+  // waits for the last sequence number of a chunk and reads the chunk's slots.
+  static constexpr int kRing = 2 * 32;
+  Counters* ring_host = nullptr;
+  Counters* ring_dev = nullptr;
   bool ctr_clean = false;  // *ctr is known to be zero (the publisher zeroed it)
   // Queued-ahead projection (small iterations, where no bucket can be oversize): the next
   // iteration's sign-hash is enqueued behind the compaction, reading N from n_next_dev, before
@@ -454,6 +460,27 @@ struct klsh_ctx {
     ctr_clean = true;
     return check_device_err();
   }
+  // Wait until the published sequence word reaches `seq` (queued batches publish one sequence
+  // number per iteration, so the word may already be past it).
+  int wait_seq(uint32_t seq) {
+    volatile uint32_t* p = pub_seq_host;
+    uint64_t spins = 0;
+    while ((int32_t)(*p - seq) < 0) {
+      __builtin_ia32_pause();
+      if ((++spins & 0xFFFu) == 0) {
+        const hipError_t q = hipStreamQuery(stream);
+        if (q == hipSuccess) {
+          std::atomic_thread_fence(std::memory_order_seq_cst);
+          if ((int32_t)(*p - seq) < 0)
+            return fail(KLSH_E_HIP, "counters not published by a finished stream");
+          break;
+        }
+        if (q != hipErrorNotReady) return fail(KLSH_E_HIP, std::string("stream: ") + hipGetErrorString(q));
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return 0;
+  }
   int check_device_err() const {
     if (h_ctr->err)
       return fail(KLSH_E_HIP, "device protocol failure (look-back wait limit), code " +
@@ -602,7 +629,9 @@ klsh_ctx* klsh_create(int device, int* err) {
   if (ok && c->zero_copy) {
     void* hp = nullptr;
     void* dp = nullptr;
-    const size_t bytes = sizeof(Counters) + 64;
+    // [published counters][sequence word, 64 B][kRing ring slots]
+    const size_t ring_at = sizeof(Counters) + 64;
+    const size_t bytes = ring_at + sizeof(Counters) * klsh_ctx::kRing;
     if (hipHostMalloc(&hp, bytes, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
         hipHostGetDevicePointer(&dp, hp, 0) == hipSuccess) {
       memset(hp, 0, bytes);
@@ -610,6 +639,8 @@ klsh_ctx* klsh_create(int device, int* err) {
       c->pub_dev = static_cast<Counters*>(dp);
       c->pub_seq_host = reinterpret_cast<uint32_t*>(static_cast<char*>(hp) + sizeof(Counters));
       c->pub_seq_dev = reinterpret_cast<uint32_t*>(static_cast<char*>(dp) + sizeof(Counters));
+      c->ring_host = reinterpret_cast<Counters*>(static_cast<char*>(hp) + ring_at);
+      c->ring_dev = reinterpret_cast<Counters*>(static_cast<char*>(dp) + ring_at);
     } else {
       if (hp) (void)hipHostFree(hp);
       c->zero_copy = false;  // fall back to copy + sync
@@ -909,6 +940,8 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
     return e;
   // many 385..896-row runs this iteration: the next one runs that class on an auxiliary stream
   ctx->mw.big896_aux = ctx->h_ctr->n_big[klsh::kBigClasses - 1] >= 64u ? 1u : 0u;
+  // no >896-row runs this iteration: the next one's launch for them is 4 workgroups
+  ctx->mw.huge_cap = ctx->h_ctr->n_huge == 0 ? 4u : 0u;
   if (ctx->h_ctr->n_over > 0) {
     std::vector<uint2> over;
     uint64_t hyp = 0;
@@ -918,6 +951,127 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
   }
   if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
   ctx->n_live = ctx->h_ctr->total;
+  return 0;
+}
+
+// ------------------------------------------------------------------ queued tail batches -----
+// Once no bucket can be oversize (N_t <= bucket_size_threshold: nestedCluster, which needs the
+// host's RNG order, cannot happen) and N_t < 2^20 (the one-launch merge and compaction), the rest
+// of the loop needs nothing from the host: every kernel of an iteration reads N_t from
+// n_next_dev, the projection finds its hyperplanes at the offset woff (each compaction advances it
+// by its own h = floor(log2 N_t), cluster.cc:194-196), the sort runs the passes of the largest h
+// ahead (passes over all-zero digits are stable identities), the threshold schedule is known.
+// Iterations are queued C at a time, two chunks in flight; every compaction publishes into its own
+// ring slot and the host reads a chunk's slots when its last sequence number is in — the trace,
+// the RNG counter and the statistics come out exactly as the per-iteration loop's.
+static bool batch_eligible(const klsh_ctx* ctx, uint64_t n, int bucket_thr, int iters_left) {
+  static const bool on = [] {
+    const char* e = getenv("KLSH_TAIL_BATCH");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!on || n < 2 || n >= (1u << 20) || iters_left < 2) return false;
+  if (bucket_thr >= 0 && n > (uint64_t)bucket_thr) return false;
+  if (!ctx->zero_copy || !ctx->ring_dev || !ctx->lb.status || ctx->phase_timing) return false;
+  if (!klsh::project_device_n_ok(ctx->d) || ctx->mw.dlist) return false;
+  if (getenv("KLSH_BUCKET_STATS") || getenv("KLSH_ITER_LOG")) return false;
+  // every queued iteration's hyperplanes resident at once
+  return (uint64_t)iters_left * (uint64_t)floor_log2(n) * (uint64_t)ctx->dp <= (64ull << 20);
+}
+
+static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, int it_end,
+                       int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
+                       uint64_t* nt_trace, klsh_stats* st,
+                       const std::function<klsh::KTime(uint64_t)>& ktime) {
+  hipStream_t s = ctx->stream;
+  constexpr int C = klsh_ctx::kRing / 2;  // iterations per chunk
+  uint64_t n_known = ctx->n_live;         // N after the last iteration the host has read
+  const int h0 = floor_log2(n_known);
+  const uint64_t k0 = *rng_counter;
+  const uint64_t need = (uint64_t)(it_end - it) * (uint64_t)h0;
+  if (!(ctx->W && ctx->w_base == seed_base && ctx->w_dp == ctx->dp && ctx->w_d == ctx->d &&
+        k0 >= ctx->w_k0 && k0 + need <= ctx->w_k0 + ctx->w_count)) {
+    KLSH_HIP(hipStreamSynchronize(s));  // a queued projection may still read the window
+    if (int e = ctx->ensure_hyperplanes(seed_base, k0, need, &st->host_ms)) return e;
+  }
+  uint32_t* n_dev = ctx->n_next_dev;
+  uint32_t* woff_dev = ctx->n_next_dev + 1;
+  KLSH_HIP(hipMemsetD32Async(n_dev, (int)(uint32_t)n_known, 1, s));
+  KLSH_HIP(hipMemsetD32Async(woff_dev, (int)(uint32_t)(k0 - ctx->w_k0), 1, s));
+  bool queued = ctx->spec_pending;  // the first projection is already on the stream
+  ctx->spec_pending = false;
+  if (!queued && !ctx->ctr_clean)
+    if (int e = ctx->reset_counters()) return e;
+  if (queued && ctx->spec_k != k0) return fail(KLSH_E_STATE, "queued projection out of step");
+
+  struct Chunk {
+    int it0, count, slot0;
+    uint32_t seq_last;
+  };
+  std::deque<Chunk> inflight;
+  int next = it, slot = 0;
+  float thr = threshold;
+  uint64_t n_max = n_known;
+  auto enqueue = [&](int count) -> int {
+    const int hb = floor_log2(n_max);  // h of every iteration of the chunk is <= hb
+    for (int c = 0; c < count; ++c, ++next) {
+      const klsh::KTime kt = ktime(ctx->kt_iter++);
+      if (!queued)
+        klsh::launch_project_device_n(ctx->rows, ctx->order, ctx->keys, (uint32_t)n_max, ctx->W,
+                                      n_dev, s, kt, woff_dev);
+      queued = false;
+      uint32_t *fk = nullptr, *fv = nullptr;
+      klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n_max, hb,
+                       ctx->hist, &fk, &fv, s, kt, n_dev);
+      ctx->mw.kt = kt;
+      klsh::launch_merge(ctx->rows, fk, fv, 0, (uint32_t)n_max, thr, bucket_size_threshold,
+                         ctx->mw, ctx->ctr, s, n_dev);
+      ctx->mw.kt = klsh::kNoTime;
+      uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
+      klsh::Publish pub{ctx->ring_dev + slot, ctx->pub_seq_dev, ++ctx->pub_seq, n_dev, woff_dev};
+      klsh::launch_compact(fv, (uint32_t)n_max, out, ctx->tile_sums, ctx->ctr, s, &pub, ctx->rc,
+                           kt, &ctx->lb, n_dev);
+      if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
+      thr -= sim_step;
+      slot = (slot + 1) % klsh_ctx::kRing;
+    }
+    KLSH_HIP(hipGetLastError());
+    return 0;
+  };
+  while (next < it_end || !inflight.empty()) {
+    while (next < it_end && inflight.size() < 2) {
+      const Chunk ch{next, std::min(C, it_end - next), slot, 0u};
+      if (int e = enqueue(ch.count)) return e;
+      inflight.push_back(ch);
+      inflight.back().seq_last = ctx->pub_seq;
+    }
+    const Chunk ch = inflight.front();
+    inflight.pop_front();
+    if (int e = ctx->wait_seq(ch.seq_last)) return e;
+    for (int c = 0; c < ch.count; ++c) {
+      const Counters cc = ctx->ring_host[(ch.slot0 + c) % klsh_ctx::kRing];
+      const uint64_t n_in = n_known;
+      if (cc.err)
+        return fail(KLSH_E_HIP, "device protocol failure (look-back wait limit), code " +
+                                    std::to_string(cc.err));
+      if (cc.n_over || n_in == 0 || cc.total == 0 || cc.total > n_in)
+        return fail(KLSH_E_STATE, "queued iteration published inconsistent counters");
+      const int h = floor_log2(n_in);
+      if (nt_trace) nt_trace[ch.it0 + c] = n_in;
+      st->iterations += 1;
+      *rng_counter += (uint64_t)h;
+      st->hyperplanes += (uint64_t)h;
+      st->sum_rows += n_in;
+      st->sum_proj_bits += n_in * (uint64_t)h;
+      st->sum_merges += n_in - cc.total;
+      if (ctx->kernel_timing && ctx->kstamp) count_class_rows(st, cc, n_in, true);
+      *ctx->h_ctr = cc;
+      n_known = cc.total;
+    }
+    n_max = n_known;  // tighter grids for the chunks queued from now on
+  }
+  threshold = thr;
+  ctx->n_live = n_known;
+  ctx->ctr_clean = true;  // every publisher zeroed the counters behind it
   return 0;
 }
 
@@ -943,6 +1097,13 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
   };
   for (int it = it_begin; it < it_end; ++it) {
     const uint64_t n = ctx->n_live;
+    if (batch_eligible(ctx, n, bucket_size_threshold, it_end - it)) {  // the rest, queued
+      const std::function<klsh::KTime(uint64_t)> kt_fn = ktime;
+      if (int e = run_batched(ctx, threshold, sim_step, it, it_end, bucket_size_threshold,
+                              seed_base, rng_counter, nt_trace, st, kt_fn))
+        return e;
+      break;
+    }
     const double t_it = iter_log ? now_ms() : 0.0;
     if (nt_trace) nt_trace[it] = n;
     st->iterations += 1;
@@ -1337,6 +1498,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   klsh_stats* st = stats ? stats : &local;
   memset(st, 0, sizeof(*st));
   st->world = (uint64_t)ctx->world();
+  ctx->mw.huge_cap = 0;  // (set per iteration from the run counts by the single-device loop)
   const int run_iters = ctx->stop_after > 0 ? std::min(iterations, ctx->stop_after) : iterations;
   if (ctx->comm)  // any bound group, world 1 included (measures the sharded machinery alone)
     return cluster_sharded(ctx, min_similarity, iterations, run_iters, bucket_size_threshold,

@@ -131,6 +131,10 @@ struct MergeWork {
   // 385..896-row runs on aux 2 instead of ahead of the >896-row runs on the main stream: set by
   // the engine when the previous iteration had many of them (C4: thousands; C2: < 10)
   uint32_t big896_aux;
+  // >896-row runs: the launch's workgroup cap (0 = one per 897 positions, at most 512).  The
+  // engine sets a small cap after an iteration without such runs: an empty launch of hundreds of
+  // 512-lane workgroups waits for CUs behind the other classes (C2: 25 ms per step for no runs)
+  uint32_t huge_cap;
   hipStream_t aux[3];
   KTime kt;                // per-class stamps of this iteration's merge launches
   hipEvent_t small_ev[2];  // HIP events around the small-run launch (nullptr: not recorded)
@@ -188,9 +192,11 @@ struct ProjectWork {
 // the device word n_dev (written by the previous compaction), n_max bounds the grid.  Only for
 // d in {8, 16, 32, 64} (project_device_n_ok).
 bool project_device_n_ok(int d);
+// woff_dev (may be null): the iteration's hyperplanes start woff_dev[0] rows after W (a batch of
+// iterations queued at once: each compaction advances it by its own h, see Publish::woff).
 void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n_max,
                              const float* W, const uint32_t* n_dev, hipStream_t s,
-                             KTime kt = kNoTime);
+                             KTime kt = kNoTime, const uint32_t* woff_dev = nullptr);
 
 // pw (may be null): the workspace that enables the matrix-core kernel for wide rows (d > 64).
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
@@ -199,15 +205,19 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
 
 // Stable LSD radix sort of (keys, vals)[0..n) on the low `bits` bits (klsh_sort.hip); ping-pong
 // buffers, *out_k/*out_v = the pair holding the result.  ws: sort_ws_words(n) words.
+// n_dev (may be null): the key count is read on the device (<= n, which sizes the grids).
 void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
                 uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s,
-                KTime kt = kNoTime);
+                KTime kt = kNoTime, const uint32_t* n_dev = nullptr);
 
 // Greedy merge (p_cluster) over every bucket run of equal key in positions [lo, hi) of
 // (key, slots), in place: survivors first in each run, kInvalid after.  Runs longer than
 // bucket_thr (>= 0) are queued to w.over (start, length) and left untouched.
+// n_dev (may be null; lo == 0 and hi < 2^20 only): the position count is read on the device
+// (<= hi, which sizes the grids).
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
-                  float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s);
+                  float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s,
+                  const uint32_t* n_dev = nullptr);
 
 // Counters handed to the host through mapped pinned memory (no copy launch, no stream sync): the
 // compaction's last workgroup writes *ctr (total filled in) to `host`, zeroes *ctr for the next
@@ -217,6 +227,10 @@ struct Publish {
   uint32_t* seq_host;
   uint32_t seq;
   uint32_t* n_next;   // device word that also receives the survivor count (may be null)
+  // device word advanced by floor(log2 n) of the compacted iteration (may be null): the next
+  // iteration's hyperplane offset when a batch of iterations is queued at once (cluster.cc:194-196
+  // draws h = floor(log2 N_t) hyperplanes per iteration)
+  uint32_t* woff = nullptr;
 };
 
 // The look-back compaction's tile status words (>= 256, zeroed once) and the epoch of its last
@@ -228,11 +242,12 @@ struct LookBack {
 
 // out[0..total) = slots[p] for p with slots[p] != kInvalid, stable; ctr->total = count.  rc (may
 // be null): the iteration's run counters, copied into *ctr (and zeroed) before the publish.  lb
-// (may be null): one launch instead of two when n fits 256 tiles.
+// (may be null): one launch instead of two when n fits 256 tiles.  n_dev (may be null; needs lb
+// and n <= 256 tiles): the slot count is read on the device (<= n, which sizes the grid).
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
                     Counters* ctr, hipStream_t s, const Publish* pub = nullptr,
                     RunCounters* rc = nullptr, KTime kt = kNoTime,
-                    const LookBack* lb = nullptr);
+                    const LookBack* lb = nullptr, const uint32_t* n_dev = nullptr);
 // Fold set `set` of blk into its totals and clear it (the end of a timed call).
 void launch_stamp_fold(KStampBlock* blk, int set, hipStream_t s);
 

@@ -61,7 +61,8 @@ __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X,
                                                     const float* __restrict__ W, int h,
                                                     uint32_t key_or,
                                                     const uint32_t* __restrict__ n_dev = nullptr,
-                                                    KTime kt = kNoTime) {
+                                                    KTime kt = kNoTime,
+                                                    const uint32_t* __restrict__ woff_dev = nullptr) {
   constexpr int QMAX = kMaxHyperplanes / 4;
   __shared__ __attribute__((aligned(16))) float4 sw[QMAX * D];
   kt_fold(kt);
@@ -70,6 +71,7 @@ __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X,
     n = *n_dev;
     if (n == 0) return;
     h = 31 - __builtin_clz(n);
+    if (woff_dev) W += (size_t)*woff_dev * dp;
   }
   const int nq = (h + 3) >> 2;
   for (int i = threadIdx.x; i < nq * D; i += 256) {
@@ -624,11 +626,12 @@ bool project_device_n_ok(int d) {
 }
 
 void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n_max,
-                             const float* W, const uint32_t* n_dev, hipStream_t s, KTime kt) {
+                             const float* W, const uint32_t* n_dev, hipStream_t s, KTime kt,
+                             const uint32_t* woff_dev) {
   if (n_max == 0) return;
   const dim3 grid((n_max + 255) / 256), block(256);
   auto go = [&](auto kern) {
-    kern<<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev, kt);
+    kern<<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev, kt, woff_dev);
   };
   switch (r.d) {
     case 8: go(k_project_pk<8, 2, 1>); break;
@@ -690,7 +693,7 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
     return;
   }
   auto go_pk = [&](auto kern) {
-    kern<<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, nullptr, kt);
+    kern<<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, nullptr, kt, nullptr);
   };
   switch (r.d) {
     case 8: go_pk(k_project_pk<8, 2, 1>); break;
@@ -768,10 +771,12 @@ __device__ __forceinline__ void collect_run_counts(Counters* ctr, RunCounters* r
 }
 
 // Publish the iteration's counters to the host (see Publish), `total` filled in.
-__device__ __forceinline__ void publish_counters(Counters* ctr, uint32_t total, const Publish& pub) {
+__device__ __forceinline__ void publish_counters(Counters* ctr, uint32_t total, const Publish& pub,
+                                                 uint32_t n_in) {
   Counters c = *ctr;
   c.total = total;
   if (pub.n_next) *pub.n_next = total;  // for an iteration already queued (device-side n)
+  if (pub.woff && n_in) *pub.woff += 31u - (uint32_t)__builtin_clz(n_in);  // h of this iteration
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&c);
   uint32_t* dst = reinterpret_cast<uint32_t*>(pub.host);
   for (int i = 0; i < (int)(sizeof(Counters) / 4); ++i) {
@@ -784,7 +789,7 @@ __device__ __forceinline__ void publish_counters(Counters* ctr, uint32_t total, 
 
 __global__ void k_publish(Counters* ctr, Publish pub, RunCounters* rc) {
   collect_run_counts(ctr, rc);
-  if (pub.host) publish_counters(ctr, ctr->total, pub);
+  if (pub.host) publish_counters(ctr, ctr->total, pub, 0u);
 }
 
 __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restrict__ slots,
@@ -830,7 +835,7 @@ __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restric
   if (blockIdx.x == gridDim.x - 1 && t == 0) {
     *total = pre[K * 4];
     collect_run_counts(ctr, rc);
-    if (pub.host) publish_counters(ctr, pre[K * 4], pub);
+    if (pub.host) publish_counters(ctr, pre[K * 4], pub, n);
   }
   kt_end(kt, KC_COMPACT);
 }
@@ -845,10 +850,13 @@ __global__ __launch_bounds__(256) void k_compact_lb(const uint32_t* __restrict__
                                                     unsigned long long* __restrict__ status,
                                                     uint32_t epoch, uint32_t* __restrict__ total,
                                                     Counters* ctr, Publish pub, RunCounters* rc,
-                                                    KTime kt) {
+                                                    KTime kt, const uint32_t* n_dev) {
   constexpr int K = kCompactTile / 256;
   __shared__ uint32_t cnt[K * 4], pre[K * 4 + 1], wsum[4];
   kt_begin(kt, KC_COMPACT);
+  // device-side n: every workgroup reads it before it publishes its status, and the last one
+  // (which rewrites the word through pub.n_next) only after every status is in
+  if (n_dev) n = *n_dev;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t T0 = blockIdx.x * (uint32_t)kCompactTile;
   uint32_t v[K];
@@ -903,15 +911,23 @@ __global__ __launch_bounds__(256) void k_compact_lb(const uint32_t* __restrict__
   if (blockIdx.x == gridDim.x - 1 && t == 0) {
     *total = pre[K * 4];
     collect_run_counts(ctr, rc);
-    if (pub.host) publish_counters(ctr, pre[K * 4], pub);
+    if (pub.host) publish_counters(ctr, pre[K * 4], pub, n);
   }
   kt_end(kt, KC_COMPACT);
 }
 
 void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* tile_sums,
                     Counters* ctr, hipStream_t s, const Publish* pub, RunCounters* rc, KTime kt,
-                    const LookBack* lb) {
+                    const LookBack* lb, const uint32_t* n_dev) {
   const Publish none{nullptr, nullptr, 0u, nullptr};
+  if (n_dev) {  // a queued iteration: the one-launch look-back compaction over <= 256 tiles
+    const uint32_t ntiles = (n + kCompactTile - 1) / kCompactTile;
+    if (!lb || !lb->status || ntiles == 0 || ntiles > 256u) return;  // (the caller checks)
+    const uint32_t epoch = ++lb->epoch;
+    k_compact_lb<<<ntiles, 256, 0, s>>>(slots, n, out, lb->status, epoch, &ctr->total, ctr,
+                                        pub ? *pub : none, rc, kt, n_dev);
+    return;
+  }
   if (n == 0) {
     (void)hipMemsetAsync(&ctr->total, 0, sizeof(uint32_t), s);
     k_publish<<<1, 1, 0, s>>>(ctr, pub ? *pub : none, rc);
@@ -921,7 +937,7 @@ void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* 
   if (lb && lb->status && ntiles <= 256u) {
     const uint32_t epoch = ++lb->epoch;
     k_compact_lb<<<ntiles, 256, 0, s>>>(slots, n, out, lb->status, epoch, &ctr->total, ctr,
-                                        pub ? *pub : none, rc, kt);
+                                        pub ? *pub : none, rc, kt, nullptr);
     return;
   }
   uint32_t* counts = tile_sums + kScanSumsWord;

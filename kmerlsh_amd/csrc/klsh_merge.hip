@@ -654,8 +654,10 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
                                                     uint32_t n, int bucket_thr, uint32_t ntiles,
                                                     uint64_t* __restrict__ hbits,
                                                     uint32_t* __restrict__ tail_ends,
-                                                    uint32_t* __restrict__ counts, KTime kt) {
+                                                    uint32_t* __restrict__ counts, KTime kt,
+                                                    const uint32_t* __restrict__ n_dev) {
   kt_begin(kt, KC_RUNS);
+  if (n_dev) n = *n_dev;  // tiles past it find no heads and count nothing
   __shared__ uint64_t hb[kRunTile / 64];
   __shared__ uint32_t lcnt[kRunRows];
   __shared__ uint32_t s_tail_end;
@@ -1943,6 +1945,7 @@ static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, 
   }();
   (void)lds_ok;
   uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
+  if (w.huge_cap) g = std::min(g, w.huge_cap);  // (the kernel strides over its list)
   switch (r.d) {
     case 8: k_merge_huge<8><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr); break;
     case 16: k_merge_huge<16><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr); break;
@@ -2460,9 +2463,11 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
 }
 
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
-                  float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s) {
+                  float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s,
+                  const uint32_t* n_dev) {
   if (hi <= lo) return;
   const uint32_t n = hi - lo;
+  if (n_dev && (lo != 0 || n >= kTailMergeMax)) return;  // (the caller checks)
   const Decider dc = make_decider(thr);
   const uint32_t ntiles = (n + kRunTile - 1) / kRunTile;
   uint32_t* counts = w.run_ws;
@@ -2470,7 +2475,7 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   // 8-byte aligned: counts + tail ends take (kRunRows + 1) * ntiles words, rounded up to even
   uint64_t* hbits = reinterpret_cast<uint64_t*>(counts + (((kRunRows + 1u) * ntiles + 1u) & ~1u));
   k_runs_count<<<ntiles, 256, 0, s>>>(key, lo, n, bucket_thr, ntiles, hbits, tail_ends, counts,
-                                      w.kt);
+                                      w.kt, n_dev);
   const bool fused = ntiles <= 256u;  // the write kernel scans the counts itself
   if (!fused) k_runs_scan<<<kRunRows, 256, 0, s>>>(counts, ntiles, w.rc);
   if (fused) k_runs_write<true><<<ntiles, 256, 0, s>>>(lo, bucket_thr, ntiles, hbits, tail_ends, counts, w);

@@ -29,10 +29,12 @@ constexpr int kSortItems = 16;
 template <int B>
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys, uint32_t n,
                                                    int shift, uint32_t ntiles,
-                                                   uint32_t* __restrict__ hist, KTime kt) {
+                                                   uint32_t* __restrict__ hist, KTime kt,
+                                                   const uint32_t* __restrict__ n_dev) {
   constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u;
   __shared__ uint32_t c[RAD];
   kt_begin(kt, KC_SORT);  // (only the first pass's launch carries kt)
+  if (n_dev) n = *n_dev;  // tiles past it count nothing
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   for (uint32_t d = t; d < RAD; d += 256) c[d] = 0u;
   const uint32_t base = blockIdx.x * kSortTile + wv * 1024u + lane;
@@ -76,8 +78,10 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
                                                       uint32_t* __restrict__ vout, uint32_t n,
                                                       int shift, uint32_t ntiles,
                                                       const uint32_t* __restrict__ hist,
-                                                      const uint32_t* __restrict__ dtot, KTime kt) {
+                                                      const uint32_t* __restrict__ dtot, KTime kt,
+                                                      const uint32_t* __restrict__ n_dev) {
   constexpr uint32_t RAD = 1u << B, MASK = RAD - 1u, PER = RAD / 256u;
+  if (n_dev) n = *n_dev;
   __shared__ uint32_t lk[kSortTile], lv[kSortTile];
   __shared__ uint32_t wc[4][RAD];  // per-wave running digit counts, then their wave prefixes
   __shared__ uint32_t ls[RAD];     // tile-local start of each digit
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
     }
   }
   __syncthreads();
-  const uint32_t m = min(kSortTile, n - T0);
+  const uint32_t m = T0 < n ? min(kSortTile, n - T0) : 0u;
   for (uint32_t e = t; e < m; e += 256) {
     const uint32_t kk = lk[e];
     const uint32_t o = gb[(kk >> shift) & MASK] + e;
@@ -172,18 +176,22 @@ uint64_t sort_ws_words(uint64_t slots) {
 template <int B>
 static void sort_pass(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo,
                       uint32_t n, int shift, uint32_t* ws, hipStream_t s, KTime kt,
-                      bool first, bool last) {
+                      bool first, bool last, const uint32_t* n_dev) {
   const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
   uint32_t* hist = ws;
   uint32_t* dtot = ws + (size_t)(1u << B) * ntiles;
-  k_sort_hist<B><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, hist, first ? kt : kNoTime);
+  k_sort_hist<B><<<ntiles, 256, 0, s>>>(ki, n, shift, ntiles, hist, first ? kt : kNoTime, n_dev);
   k_sort_dscan<<<1u << B, 256, 0, s>>>(hist, ntiles, dtot);
   k_sort_scatter<B><<<ntiles, 256, 0, s>>>(ki, vi, ko, vo, n, shift, ntiles, hist, dtot,
-                                           last ? kt : kNoTime);
+                                           last ? kt : kNoTime, n_dev);
 }
 
+// With n_dev the passes are those of `bits` whatever the device count turns out to be: a queued
+// iteration's keys have h <= bits significant bits, and a pass over digits that are all zero is a
+// stable identity, so the order is the same as a sort on h bits.
 void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, int bits,
-                uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s, KTime kt) {
+                uint32_t* ws, uint32_t** out_k, uint32_t** out_v, hipStream_t s, KTime kt,
+                const uint32_t* n_dev) {
   uint32_t *ki = k0, *vi = v0, *ko = k1, *vo = v1;
   if (n > 1 && bits > 0) {
     // P passes of B-bit digits: 1..10 bits one pass, 11..20 two, 21..30 three, 31..32 four
@@ -192,9 +200,9 @@ void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t
     for (int p = 0; p < P; ++p) {
       const int shift = p * B;
       const bool first = p == 0, last = p == P - 1;
-      if (B == 8) sort_pass<8>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last);
-      else if (B == 9) sort_pass<9>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last);
-      else sort_pass<10>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last);
+      if (B == 8) sort_pass<8>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last, n_dev);
+      else if (B == 9) sort_pass<9>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last, n_dev);
+      else sort_pass<10>(ki, vi, ko, vo, n, shift, ws, s, kt, first, last, n_dev);
       std::swap(ki, ko);
       std::swap(vi, vo);
     }
