@@ -307,6 +307,10 @@ def kernel_rooflines(config, stats, steps, d, trace):
     import math
 
     register = d in (8, 16, 32, 64)
+    # the projection reads the fp16 row image (2d bytes a row) where the engine keeps one
+    # (d = 16, 32, 64; KLSH_SHADOW=0 turns it off); its close calls re-read the f32 row (k_project_fix)
+    shadow = d in (16, 32, 64) and os.environ.get("KLSH_SHADOW", "1") != "0"
+    row_bytes = 2 * d if shadow else 4 * d
     kern = {c: {f: sum(s["kern"][c][f] for s in stats) for f in ("ms", "launches", "rows", "runs")}
             for c in stats[0]["kern"]}
     merges_small = sum(s["small_iter_merges"] for s in stats)
@@ -319,12 +323,14 @@ def kernel_rooflines(config, stats, steps, d, trace):
         if not k["launches"] or k["ms"] <= 0:
             continue
         rows, runs = k["rows"], k["runs"]
-        b = {"project": rows * (4 * d + 8), "sort": sort_bytes, "runs": rows * 4 + runs * 8,
+        b = {"project": rows * (row_bytes + 8), "sort": sort_bytes, "runs": rows * 4 + runs * 8,
              "small": rows * (4 * d + 4) + merges_small * (4 * d + 20),
              "tail": rows * (4 * d + 8), "compact": rows * 12}.get(c, rows * (4 * d + 20))
         avg = k["ms"] / k["launches"]
         ach = (b / k["launches"]) / (avg * 1e-3) / 1e9
         name = (KERNEL_NAMES if register or c not in WIDE_NAMES else WIDE_NAMES)[c].format(d=d)
+        if c == "project" and shadow:
+            name = f"k_project_h16<{d}>"
         pmc = pmc_traffic(config, c) or pmc_traffic(config, {"project": "k_project",
                                                              "small": "k_merge_small"}.get(c, ""))
         e = {"kernel": name, "class": c, "bound": "hbm", "achieved": round(ach, 2),
@@ -355,7 +361,20 @@ def kernel_rooflines(config, stats, steps, d, trace):
                          avg_launch_ms=ev_avg, ms_per_step=ev_ms / steps, timing="hip_events")
         if c == "project":
             bits = sum(s["sum_proj_bits"] for s in stats)
-            if register:
+            if shadow:
+                # the fp16-image screen: S = X~ (w_hi + w_lo)^T, 2 f16 MFMA products per product
+                fl = 2 * 2.0 * bits * d / k["launches"]
+                e["mfma"] = {"achieved": round(fl / (avg * 1e-3) / 1e12, 2),
+                             "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                             "note": "fp16 row image x w split into fp16 hi + lo on "
+                                     "v_mfma_f32_32x32x16_f16 (2 products per product, dense f16 "
+                                     "peak); close calls settled in the kernel on the f32 row"}
+                e["mfma"]["frac"] = round(e["mfma"]["achieved"] / BF16_DENSE_TFLOPS, 5)
+                fixed = sum(s.get("proj_fix_pairs", 0) for s in stats)
+                e["close_calls"] = {"pairs": fixed / steps, "frac_of_pairs": fixed / max(1, bits),
+                                    "note": "row-hyperplane pairs per step the screen left to the "
+                                            "exact f32 chains"}
+            elif register:
                 # one v_pk_mul + one v_pk_add per two row-hyperplane MACs (bit-exactness forbids
                 # fusing): 256 CU x 4 SIMD x 32 lanes x 2 flop x 2.4 GHz / 2 = 78.6 Tflop/s
                 fl = 2.0 * bits * d / k["launches"]

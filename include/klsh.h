@@ -90,6 +90,9 @@ typedef struct klsh_stats {
   uint64_t small_iter_merges;
   /* per kernel class (single-GPU loop; option "kernel_timing", default on) */
   klsh_kstat kern[KLSH_KCLASSES];
+  /* certified projection screens (d > 64, or the fp16 row image at d = 16, 32, 64): the
+   * (row, hyperplane) pairs the screen could not call and the exact chains settled */
+  uint64_t proj_fix_pairs;
 } klsh_stats;
 
 /* ---- lifetime ------------------------------------------------------------------------------- */

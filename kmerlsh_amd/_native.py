@@ -77,6 +77,7 @@ class KlshStats(ctypes.Structure):
         ("small_rows", ctypes.c_uint64),
         ("small_iter_merges", ctypes.c_uint64),
         ("kern", KlshKstat * KCLASSES),
+        ("proj_fix_pairs", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

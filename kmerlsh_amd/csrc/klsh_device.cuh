@@ -157,6 +157,24 @@ __device__ __forceinline__ float norm_mem(const float* a, int d) {
 }
 
 // Member list of `cur` goes in front of `cand`'s (funcAB.cc:51-55: ids = ids_cur ++ ids_cand).
+// Row stores of the merge kernels: x and, when kept, its fp16 image (Rows::xh) — every write of
+// a row goes through these, so the projection's screen always reads fp16(x).  `at`: float index
+// (slot * dp + column), a multiple of 4 for store_row4.
+__device__ __forceinline__ void store_row4(const Rows& r, size_t at, float4 v) {
+  *reinterpret_cast<float4*>(r.x + at) = v;
+  if (r.xh) {
+    const _Float16 h4[4] = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+    *reinterpret_cast<uint2*>(r.xh + at) = *reinterpret_cast<const uint2*>(h4);
+  }
+}
+__device__ __forceinline__ void store_row1(const Rows& r, size_t at, float v) {
+  r.x[at] = v;
+  if (r.xh) {
+    const _Float16 hv = (_Float16)v;
+    r.xh[at] = *reinterpret_cast<const uint16_t*>(&hv);
+  }
+}
+
 __device__ __forceinline__ void link_members(const Rows& r, uint32_t cur, uint32_t cand) {
   const uint32_t ca = r.cnt[cur], cb = r.cnt[cand];
   r.nxt[r.tail[cur]] = r.head[cand];

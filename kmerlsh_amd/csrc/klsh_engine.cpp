@@ -179,6 +179,13 @@ struct klsh_ctx {
   int spec_ev = 0;
   bool zero_copy = true;
   klsh::RunCounters* rc = nullptr;  // run-list counters (device, one 128-B line each)
+  // fp16 image of the rows for the projection's screen (Rows::xh; KLSH_SHADOW=0: off); every row
+  // store of the merge kernels writes it too (store_row4 / store_row1)
+  bool shadow_on = [] {
+    const char* e = getenv("KLSH_SHADOW");
+    return !(e && atoi(e) == 0);
+  }();
+  uint16_t* xh_alloc = nullptr;
 
   ~klsh_ctx() { release(); }
 
@@ -263,6 +270,8 @@ struct klsh_ctx {
     for (auto& c : mw.cls) dfree(c);
     dfree(kstamp);
     dfree(lb.status);
+    dfree(xh_alloc);
+    rows.xh = nullptr;
     cap_slots = cap_members = 0;
     cap_dp = 0;
     drop_snapshot();
@@ -313,6 +322,7 @@ struct klsh_ctx {
       dp = dp_;
       rows.d = d;
       rows.dp = dp;
+      rows.xh = klsh::shadow_width_ok(d) ? xh_alloc : nullptr;
       drop_snapshot();
       return 0;
     }
@@ -333,6 +343,12 @@ struct klsh_ctx {
         (e = dalloc(&mw.huge, s / 897 + 64))) {
       release_state();
       return e;
+    }
+    if (shadow_on && klsh::shadow_width_ok(d_)) {  // (in the large-buffer group: see below)
+      if ((e = dalloc(&xh_alloc, s * dp_))) {
+        release_state();
+        return e;
+      }
     }
     for (int c = 0; c < klsh::kGroupClasses; ++c) {
       if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s)))) {
@@ -378,6 +394,7 @@ struct klsh_ctx {
     dp = dp_;
     rows.d = d;
     rows.dp = dp;
+    rows.xh = klsh::shadow_width_ok(d) ? xh_alloc : nullptr;
     return 0;
   }
 
@@ -707,6 +724,8 @@ int klsh_load_rows(klsh_ctx* ctx, const float* rows, uint64_t n, int d,
   KLSH_HIP(hipStreamSynchronize(s));
   ctx->slots = n;
   ctx->members = m;
+  klsh::launch_shadow_build(ctx->rows, ctx->slots, s);
+  KLSH_HIP(hipGetLastError());
   ctx->n_live = n;
   ctx->loaded = true;
   return 0;
@@ -768,6 +787,8 @@ int klsh_load_counts(klsh_ctx* ctx, const uint16_t* counts, uint64_t n_total,
   for (uint64_t i = 0; i < bs; ++i) ctx->ids[i] = batch_offset + i;
   ctx->slots = bs;
   ctx->members = bs;
+  klsh::launch_shadow_build(ctx->rows, ctx->slots, s);
+  KLSH_HIP(hipGetLastError());
   ctx->n_live = bs ? ctx->h_ctr->total : 0;
   ctx->loaded = true;
   return 0;
@@ -816,6 +837,8 @@ int klsh_restore(klsh_ctx* ctx) {
   KLSH_HIP(hipMemcpyAsync(ctx->rows.nxt, sn.nxt, 4 * m, hipMemcpyDeviceToDevice, st));
   KLSH_HIP(hipMemcpyAsync(ctx->order, sn.order, 4 * sn.n_live, hipMemcpyDeviceToDevice, st));
   KLSH_HIP(hipStreamSynchronize(st));
+  klsh::launch_shadow_build(ctx->rows, ctx->slots, st);  // (rebuilt, not snapshotted)
+  KLSH_HIP(hipGetLastError());
   ctx->n_live = sn.n_live;
   return 0;
 }
@@ -1017,7 +1040,7 @@ static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, 
       const klsh::KTime kt = ktime(ctx->kt_iter++);
       if (!queued)
         klsh::launch_project_device_n(ctx->rows, ctx->order, ctx->keys, (uint32_t)n_max, ctx->W,
-                                      n_dev, s, kt, woff_dev);
+                                      n_dev, s, kt, woff_dev, &ctx->pw);
       queued = false;
       uint32_t *fk = nullptr, *fv = nullptr;
       klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n_max, hb,
@@ -1180,7 +1203,8 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
       const int ne = e0 == 0 ? 6 : 0;
       if (rec) KLSH_HIP(hipEventRecord(ctx->ev[ne], s));
       klsh::launch_project_device_n(ctx->rows, next_order, ctx->keys, (uint32_t)n,
-                                    ctx->hyperplane_ptr(k_next), ctx->n_next_dev, s, ktime(j + 1));
+                                    ctx->hyperplane_ptr(k_next), ctx->n_next_dev, s, ktime(j + 1),
+                                    nullptr, &ctx->pw);
       KLSH_HIP(hipGetLastError());
       if (rec) KLSH_HIP(hipEventRecord(ctx->ev[ne + 1], s));
       ctx->spec_pending = true;
@@ -1499,6 +1523,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   memset(st, 0, sizeof(*st));
   st->world = (uint64_t)ctx->world();
   ctx->mw.huge_cap = 0;  // (set per iteration from the run counts by the single-device loop)
+  ctx->mw.dlist = nullptr;
   const int run_iters = ctx->stop_after > 0 ? std::min(iterations, ctx->stop_after) : iterations;
   if (ctx->comm)  // any bound group, world 1 included (measures the sharded machinery alone)
     return cluster_sharded(ctx, min_similarity, iterations, run_iters, bucket_size_threshold,
@@ -1532,6 +1557,19 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   // The survivor counters are published by the compaction's last workgroup, which need not be
   // the last to finish writing ctx->order: drain the stream before klsh_count/klsh_result read it.
   KLSH_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->pw.ws) {  // pairs the certified projection screens left to the exact chains
+    // ws[4..6): the wide-row fix-up kernel's total; ws[32..64): the fp16 screen's 16 counters
+    uint32_t w[64];
+    KLSH_HIP(hipMemcpy(w, ctx->pw.ws, sizeof(w), hipMemcpyDeviceToHost));
+    unsigned long long fixed = 0, part = 0;
+    for (int i : {4, 32, 34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62}) {
+      memcpy(&part, w + i, sizeof(part));
+      fixed += part;
+    }
+    KLSH_HIP(hipMemset(ctx->pw.ws + 4, 0, 8));
+    KLSH_HIP(hipMemset(ctx->pw.ws + 32, 0, 128));
+    st->proj_fix_pairs = fixed;
+  }
   st->n_final = ctx->n_live;
   st->wall_ms = now_ms() - t_start;
   if (getenv("KLSH_MERGE_PROF")) klsh::merge_prof_dump(stderr);

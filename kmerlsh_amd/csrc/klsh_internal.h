@@ -154,7 +154,14 @@ struct Rows {
   uint32_t* nxt;   // [members] next member node (kNil = end)
   int d;
   int dp;
+  // [slots][dp] fp16 image of x (round to nearest; may be null): the projection's certified
+  // screen reads it instead of x (half the bytes of the row gather).  Kept equal to fp16(x):
+  // rebuilt after a load / restore, written with x by every merge store (store_row4/store_row1)
+  // and by the sharded delta apply.
+  uint16_t* xh = nullptr;
 };
+// The fp16 image is kept for these widths (the matrix-core screen takes 16 columns per step).
+inline bool shadow_width_ok(int d) { return d == 16 || d == 32 || d == 64; }
 
 // The merge test of cluster.cc:68-69 as a threshold on the quotient.  The reference computes
 // sim = dot / (sqrtf(|a|^2) * sqrtf(|b|^2)); dist = 1 - sim; and merges when 1 - dist >= thr.
@@ -185,6 +192,7 @@ struct ProjectWork {
   uint32_t* ws;
   uint32_t cap;
 };
+constexpr uint32_t kH16Grid = 8192;  // workgroups of the fp16-image screen, at most
 
 // ---- launch wrappers (all asynchronous on `s`) ------------------------------------------------
 // keys[p] = sign-hash of row slots[p] against h hyperplanes W (h x dp), OR'ed with key_or.
@@ -196,7 +204,8 @@ bool project_device_n_ok(int d);
 // iterations queued at once: each compaction advances it by its own h, see Publish::woff).
 void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n_max,
                              const float* W, const uint32_t* n_dev, hipStream_t s,
-                             KTime kt = kNoTime, const uint32_t* woff_dev = nullptr);
+                             KTime kt = kNoTime, const uint32_t* woff_dev = nullptr,
+                             const ProjectWork* pw = nullptr);
 
 // pw (may be null): the workspace that enables the matrix-core kernel for wide rows (d > 64).
 void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
@@ -259,6 +268,9 @@ void launch_convert(const Rows& r, const uint16_t* counts, uint32_t bs, const fl
 
 // Sequential norms nrm[slot] for slots [0, n) (after a load).
 void launch_norms(const Rows& r, uint32_t n, hipStream_t s);
+// r.xh = fp16(r.x) for slots [0, n).
+void launch_shadow_build(const Rows& r, uint64_t n, hipStream_t s);
+
 
 // out[i*d + k] = x[order[i]][k] (compact result rows).
 void launch_gather_rows(const Rows& r, const uint32_t* order, uint32_t n, float* out,

@@ -435,6 +435,215 @@ __global__ __launch_bounds__(256) void k_project_mfma(const float* __restrict__ 
   }
 }
 
+// The projection from the fp16 row image (Rows::xh), certified.  x~ = fp16(x) is read (2d bytes a
+// row, half the f32 row gather) and S = x~ . w is taken on v_mfma_f32_32x32x16_f16 with w split
+// into fp16 hi + lo (two MFMAs per 16 columns; x~ needs no split).  Against the reference's
+// sequential f32 sum s of the f32 row (hash/lshash.cc:44-51):
+//   |S - s| <= |S - x~.w|        w split residual 2^-22 |w_k| (+ 2^-25 absolute where w_lo is
+//                                 subnormal) and the MFMA's f32 sums, (17 + 2 ceil(d/16)) 2^-23
+//            + |x~.w - x.w|      fp16 rounding of x: 2^-11 |x_k| (+ 2^-25 absolute, subnormals)
+//            + |x.w - s|         the reference's own (d + 1) 2^-24
+// summed over k with Cauchy-Schwarz: <= eps |w||x| + abs_c (|w| + |x~|) (h16_eps / h16_abs, with
+// 1.5x headroom; |x| <= 1.001 |x~| covers the 2^-11).  Signs with |S| above the bound are the
+// reference's bits; the rest (fp16 overflow, NaN, |S| within the bound: ~0.5 % of the
+// row-hyperplane pairs at d = 64) go to the fix-up list (k_project_fix: the exact chains on the
+// f32 row).  Layout as k_project_mfma: 32 rows x 32 hyperplanes per wave, one ballot per
+// accumulator register; the next group's rows are loaded during the current group.
+typedef _Float16 ph16x8 __attribute__((ext_vector_type(8)));
+
+float h16_eps(int d) {
+  const float ks = (float)((d + 15) / 16);
+  return 1.5f * (0x1p-11f + 0x1p-22f + (17.0f + 2.0f * ks) * 0x1p-23f + (float)(d + 1) * 0x1p-24f);
+}
+float h16_abs(int d) { return 1.5f * 2.0f * 0x1p-25f * std::sqrt((float)d); }
+
+// Lane-owned rows: every lane loads one whole fp16 row (2d bytes), then one v_permlane32_swap per
+// dword turns the chunk pair (cols 16s..16s+7, 16s+8..16s+15) of lanes L and L + 32 into the
+// B operands of two 32-row tiles (lanes 0-31 keep their low chunk and take lane L + 32's, lanes
+// 32-63 keep their high chunk and take lane L - 32's).  The product is S^T = W X^T, so lane L
+// holds, for row L & 31 of a tile, the 16 hyperplanes (i&3) + 8(i>>2) + 4(L>>5): the key bits
+// of a row are lane-local (two lanes, one swap to combine), no ballots.  Close calls go to this
+// workgroup's segment and are settled at the end of the kernel by the same workgroup, one lane
+// per listed row: the f32 row loaded once, the reference's sequential chain (hash/lshash.cc:44-51,
+// mul then add, never fused) per flagged hyperplane from the f32 hyperplanes in LDS.
+typedef _Float16 ph16x2 __attribute__((ext_vector_type(2)));
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_project_h16(const uint16_t* __restrict__ XH,
+                                                     const float* __restrict__ X, int dp,
+                                                     const uint32_t* __restrict__ slots,
+                                                     uint32_t* __restrict__ keys, uint32_t n,
+                                                     const float* __restrict__ W, int h,
+                                                     uint32_t key_or, float eps, float abs_c,
+                                                     ProjectWork pw, uint32_t segcap, KTime kt,
+                                                     const uint32_t* __restrict__ n_dev,
+                                                     const uint32_t* __restrict__ woff_dev) {
+  constexpr int KS = D / 16;  // k-steps of 16 columns
+  __shared__ ph16x8 sa[2][KS][64];  // A fragments (w_hi, w_lo) of every lane, per k-step
+  __shared__ __attribute__((aligned(16))) float swf[32 * D];  // f32 hyperplanes (exact chains)
+  __shared__ float swn[32];         // |w_j| (bounds)
+  __shared__ uint32_t s_cnt;        // entries of this workgroup's fix-up segment
+  __shared__ uint32_t s_close;      // close calls (statistics)
+  kt_fold(kt);
+  kt_begin(kt, KC_PROJECT);
+  if (n_dev) {
+    n = *n_dev;
+    h = n ? 31 - __builtin_clz(n) : 0;
+    if (woff_dev) W += (size_t)*woff_dev * dp;
+  }
+  const uint32_t t = threadIdx.x, lane = t & 63u, hh = lane >> 5;
+  for (int e = (int)t; e < 32 * D; e += 256) {
+    const int j = e / D, k = e % D;
+    swf[e] = j < h ? W[(size_t)j * dp + k] : 0.0f;
+  }
+  if (t == 0) s_cnt = s_close = 0u;
+  __syncthreads();
+  if (t < 32) {
+    float a = 0.0f;
+    for (int k = 0; k < D; ++k) a += swf[t * D + k] * swf[t * D + k];
+    swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;  // a bound: the hardware sqrt (1 ulp) suffices
+  }
+  // A fragment of lane L at k-step s: hyperplane L & 31, columns 16s + 8(L >> 5) + 0..7, split
+  for (int e = (int)t; e < KS * 64; e += 256) {
+    const int sk = e >> 6, L = e & 63, j = L & 31, k0 = 16 * sk + 8 * (L >> 5);
+    ph16x8 hi8, lo8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float w = swf[j * D + k0 + q];
+      const _Float16 hi = (_Float16)w;
+      hi8[q] = hi;
+      lo8[q] = (_Float16)(w - (float)hi);  // w - hi is exact in f32
+    }
+    sa[0][sk][L] = hi8;
+    sa[1][sk][L] = lo8;
+  }
+  __syncthreads();
+  const uint32_t wv = t >> 6;
+  const uint32_t step = gridDim.x * 256u;
+  uint32_t g0 = (blockIdx.x * 4u + wv) * 64u;
+  uint32_t sl = g0 + lane < n ? slots[g0 + lane] : 0u;
+  uint4* seg = reinterpret_cast<uint4*>(pw.fix) + (size_t)blockIdx.x * segcap;
+  for (; g0 < n; g0 += step) {
+    ph16x8 xr[2 * KS];  // the lane's row, 8 columns per chunk
+    {
+      const uint16_t* src = XH + (size_t)sl * dp;
+#pragma unroll
+      for (int c = 0; c < 2 * KS; ++c) xr[c] = *reinterpret_cast<const ph16x8*>(src + 8 * c);
+    }
+    sl = g0 + step + lane < n ? slots[g0 + step + lane] : 0u;  // the next iteration's slot
+    float ss = 0.0f;  // |x~|^2 of the lane's row (a bound only)
+#pragma unroll
+    for (int c = 0; c < 2 * KS; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const ph16x2 v = {xr[c][e], xr[c][e + 1]};
+        ss = __builtin_amdgcn_fdot2(v, v, ss, false);
+      }
+    const float xn = __builtin_amdgcn_sqrtf(ss) * 1.001f;  // >= |x| (or inf / NaN)
+    pf32x16 accA, accB;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) accA[i] = accB[i] = 0.0f;
+#pragma unroll
+    for (int sk = 0; sk < KS; ++sk) {
+      uint4 a = *reinterpret_cast<const uint4*>(&xr[2 * sk]);
+      uint4 b = *reinterpret_cast<const uint4*>(&xr[2 * sk + 1]);
+      auto p0 = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+      auto p1 = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+      auto p2 = __builtin_amdgcn_permlane32_swap(a.z, b.z, false, false);
+      auto p3 = __builtin_amdgcn_permlane32_swap(a.w, b.w, false, false);
+      a = make_uint4(p0[0], p1[0], p2[0], p3[0]);  // tile A (rows of lanes 0-31)
+      b = make_uint4(p0[1], p1[1], p2[1], p3[1]);  // tile B (rows of lanes 32-63)
+      const ph16x8 fa = *reinterpret_cast<const ph16x8*>(&a);
+      const ph16x8 fb = *reinterpret_cast<const ph16x8*>(&b);
+      const ph16x8 wh = sa[0][sk][lane], wl = sa[1][sk][lane];
+      accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, fa, accA, 0, 0, 0);
+      accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, fb, accB, 0, 0, 0);
+      accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, fa, accA, 0, 0, 0);
+      accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, fb, accB, 0, 0, 0);
+    }
+    // acc[i] = S[hyperplane (i&3) + 8(i>>2) + 4hh][tile row lane & 31]; tile A's row R is lane
+    // R's own, tile B's lane 32 + R's
+    const float xo = __shfl_xor(xn, 32, 64);
+    uint32_t bits[2], amb[2];
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+      const float xr_n = (tb == 0) == (hh == 0) ? xn : xo;  // |x~| of the tile row
+      const float c1 = eps * xr_n + abs_c, c2 = abs_c * xr_n;
+      const bool huge = !(xr_n <= 0x1p100f);  // NaN, inf (fp16 overflow): exact chains
+      uint32_t bt = 0u, am = 0u;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int j = (i & 3) + 8 * (i >> 2) + 4 * (int)hh;
+        if (j < h) {
+          const float sv = tb ? accB[i] : accA[i];
+          const float bound = swn[j] * c1 + c2;
+          bt |= (sv >= 0.0f ? 1u : 0u) << j;
+          am |= ((!(__builtin_fabsf(sv) > bound) || huge) ? 1u : 0u) << j;
+        }
+      }
+      bits[tb] = bt | (uint32_t)__shfl_xor((int)bt, 32, 64);
+      amb[tb] = am | (uint32_t)__shfl_xor((int)am, 32, 64);
+    }
+    const uint32_t row = g0 + lane;  // lane L writes tile A row L (L < 32) / tile B row L - 32
+    const uint32_t mb = hh ? bits[1] : bits[0], ma = hh ? amb[1] : amb[0];
+    if (row < n) {
+      uint32_t key_bits = mb & ~ma;  // close calls start at 0: the fix-up sets the ones >= 0
+      bool done = true;
+      if (ma) {  // to this workgroup's fix-up segment (settled below; in place if it is full)
+        atomicAdd(&s_close, (uint32_t)__popc(ma));
+        const uint32_t at = atomicAdd(&s_cnt, 1u);
+        if (at < segcap) {
+          seg[at] = make_uint4(row, ma, key_bits, 0u);
+          done = false;
+        } else {
+          const float* x = X + (size_t)slots[row] * dp;
+          uint32_t a = ma;
+          while (a) {
+            const int j = __builtin_ctz(a);
+            a &= a - 1u;
+            float sd = 0.0f;  // -ffp-contract=off: the reference's mul, add order
+            for (int k = 0; k < D; ++k) sd = sd + swf[j * D + k] * x[k];
+            if (sd >= 0.0f) key_bits |= 1u << j;
+          }
+        }
+      }
+      // hyperplane 0 is the key's most significant bit
+      if (done) keys[row] = (h > 0 ? (__builtin_bitreverse32(key_bits) >> (32 - h)) : 0u) | key_or;
+    }
+  }
+  __syncthreads();
+  // the close calls of this workgroup's rows
+  const uint32_t cnt = min(s_cnt, segcap);
+  for (uint32_t e = t; e < cnt; e += 256) {
+    const uint4 f = seg[e];
+    const float* x = X + (size_t)slots[f.x] * dp;
+    float4 u[D / 4];
+#pragma unroll
+    for (int q = 0; q < D / 4; ++q) u[q] = *reinterpret_cast<const float4*>(x + 4 * q);
+    uint32_t key_bits = f.z, a = f.y;
+    while (a) {
+      const int j = __builtin_ctz(a);
+      a &= a - 1u;
+      const float* w = swf + j * D;
+      float sd = 0.0f;
+#pragma unroll
+      for (int q = 0; q < D / 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(w + 4 * q);
+        sd = sd + v.x * u[q].x;
+        sd = sd + v.y * u[q].y;
+        sd = sd + v.z * u[q].z;
+        sd = sd + v.w * u[q].w;
+      }
+      if (sd >= 0.0f) key_bits |= 1u << j;
+    }
+    keys[f.x] = (h > 0 ? (__builtin_bitreverse32(key_bits) >> (32 - h)) : 0u) | key_or;
+  }
+  if (t == 0 && s_close)  // the call's running total (16 spread 64-bit counters at ws[32..64))
+    atomicAdd(reinterpret_cast<unsigned long long*>(pw.ws + 32 + 2 * (blockIdx.x & 15u)),
+              (unsigned long long)s_close);
+  kt_end(kt, KC_PROJECT);
+}
+
 // Wide rows (d > 64, any d): the same certified matrix-core screen with the hyperplanes pre-split
 // into bf16 hi/lo fragments in LDS ([k-step][lane] 32 B each: 64 KB at d = 512) and the row
 // streamed 64 columns at a time (8 loads in flight per lane).  The pairs the screen cannot call
@@ -581,9 +790,16 @@ __global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X
                                                      const uint32_t* __restrict__ slots,
                                                      uint32_t* __restrict__ keys,
                                                      const float* __restrict__ W, int h,
-                                                     ProjectWork pw, KTime kt) {
+                                                     ProjectWork pw, KTime kt,
+                                                     const uint32_t* __restrict__ n_dev = nullptr,
+                                                     const uint32_t* __restrict__ woff_dev = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float fw[];  // the h hyperplanes, stride dp
   __shared__ uint32_t s_last;
+  if (n_dev) {  // a queued iteration: h and the hyperplane offset from the device
+    const uint32_t n = *n_dev;
+    h = n ? 31 - __builtin_clz(n) : 0;
+    if (woff_dev) W += (size_t)*woff_dev * dp;
+  }
   const uint32_t count = min(pw.ws[0], pw.cap);
   if (blockIdx.x * 256u < count)
     for (int i = (int)threadIdx.x; i < h * dp; i += 256) fw[i] = W[i];
@@ -615,10 +831,34 @@ __global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X
   if (threadIdx.x == 0) s_last = atomicAdd(&pw.ws[1], 1u) == gridDim.x - 1 ? 1u : 0u;
   __syncthreads();
   if (s_last && threadIdx.x == 0) {
+    // the call's running total of settled pairs (ws[4..5], read by the engine's statistics)
+    atomicAdd(reinterpret_cast<unsigned long long*>(pw.ws + 4), (unsigned long long)pw.ws[0]);
     atomicExch(&pw.ws[0], 0u);
     atomicExch(&pw.ws[1], 0u);
   }
   kt_end(kt, KC_PROJECT);  // the screen + fix-up span (k_project_mfma_wide stamps the start)
+}
+
+// The fp16-image screen (its close calls settled in the wave).  h: the iteration's h, or (n_dev
+// given) ignored: the kernel derives it from the device count.
+static void launch_h16(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
+                       const float* W, int h, uint32_t key_or, hipStream_t s,
+                       const ProjectWork& pw, KTime kt, const uint32_t* n_dev,
+                       const uint32_t* woff_dev) {
+  const uint32_t grid = std::min<uint32_t>((n + 255) / 256, kH16Grid);
+  const uint32_t segcap = (pw.cap / 2) / grid;  // 16-B fix-up entries per workgroup
+  const float eps = h16_eps(r.d), abs_c = h16_abs(r.d);
+  auto go = [&](auto screen) {
+    screen<<<grid, 256, 0, s>>>(r.xh, r.x, r.dp, slots, keys, n, W, h, key_or, eps, abs_c, pw,
+                                segcap, kt, n_dev, woff_dev);
+  };
+  if (r.d == 64) go(k_project_h16<64>);
+  else if (r.d == 32) go(k_project_h16<32>);
+  else go(k_project_h16<16>);
+}
+
+static bool h16_ok(const Rows& r, const ProjectWork* pw) {
+  return pw && r.xh && shadow_width_ok(r.d);
 }
 
 bool project_device_n_ok(int d) {
@@ -627,8 +867,13 @@ bool project_device_n_ok(int d) {
 
 void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n_max,
                              const float* W, const uint32_t* n_dev, hipStream_t s, KTime kt,
-                             const uint32_t* woff_dev) {
+                             const uint32_t* woff_dev, const ProjectWork* pw) {
   if (n_max == 0) return;
+  if (h16_ok(r, pw)) {
+    const int hmax = 31 - __builtin_clz(n_max);  // h of the device count is <= this
+    launch_h16(r, slots, keys, n_max, W, hmax, 0u, s, *pw, kt, n_dev, woff_dev);
+    return;
+  }
   const dim3 grid((n_max + 255) / 256), block(256);
   auto go = [&](auto kern) {
     kern<<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n_max, W, 0, 0u, n_dev, kt, woff_dev);
@@ -679,6 +924,10 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
       k_project_fix<<<1024, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
       return;
     }
+  }
+  if (h16_ok(r, pw) && h > 0 && !project_mfma_requested()) {
+    launch_h16(r, slots, keys, n, W, h, key_or, s, *pw, kt, nullptr, nullptr);
+    return;
   }
   if (project_mfma_requested() && (r.d == 16 || r.d == 32 || r.d == 64)) {
     const uint32_t groups = (n + 127) / 128;  // 4 waves x 32 rows per workgroup per step
@@ -1002,6 +1251,23 @@ __global__ __launch_bounds__(256) void k_norms(Rows r, uint32_t n) {
 void launch_norms(const Rows& r, uint32_t n, hipStream_t s) {
   if (n) k_norms<<<(n + 255) / 256, 256, 0, s>>>(r, n);
 }
+
+// fp16 image of the rows (round to nearest even; |x| >= 65520 becomes inf, which the screen
+// sends to the exact chains)
+__global__ __launch_bounds__(256) void k_shadow_build(Rows r, uint64_t words) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256ull) {
+    const float4 v = reinterpret_cast<const float4*>(r.x)[i];
+    const _Float16 h4[4] = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+    reinterpret_cast<uint2*>(r.xh)[i] = *reinterpret_cast<const uint2*>(h4);
+  }
+}
+
+void launch_shadow_build(const Rows& r, uint64_t n, hipStream_t s) {
+  const uint64_t words = n * (uint64_t)r.dp / 4;  // float4 groups (dp is a multiple of 4)
+  if (!r.xh || !words) return;
+  k_shadow_build<<<(uint32_t)std::min<uint64_t>(16384, (words + 255) / 256), 256, 0, s>>>(r, words);
+}
+
 
 // One row per wave-pass, grid-strided: a launch's work-items must stay below 2^32 (C5's result,
 // 9.98M rows x 512, is 5.1e9 floats — a thread per float wrapped and dropped 2^32 of them).

@@ -391,7 +391,7 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
     if (valid && size < b) slots[p + g] = g < size ? slot : kInvalid;
     if (valid && dirty) {  // a rewritten row sits at a position below every merge after it
       const float* src = lds + (gbase + rid) * ST;
-      float* xo = r.x + (size_t)slot * r.dp;
+      const size_t xo = (size_t)slot * r.dp;
       float nv = 0.0f;  // its exact sequential norm (distance.cc:33-34)
 #pragma unroll
       for (int k = 0; k < D; k += 4) {
@@ -400,7 +400,7 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
         nv = nv + v.y * v.y;
         nv = nv + v.z * v.z;
         nv = nv + v.w * v.w;
-        *reinterpret_cast<float4*>(xo + k) = v;
+        store_row4(r, xo + k, v);
       }
       r.nrm[slot] = nv;
       r.cnt[slot] = cnt;
@@ -468,7 +468,7 @@ __device__ __forceinline__ void pair_batch(const uint2* __restrict__ list, uint3
       const uint32_t ca = r.cnt[s1], cb = r.cnt[s0];  // current = row 1, candidate = row 0
       const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
       float nn = 0.0f;
-      float* xo = r.x + (size_t)s0 * r.dp;
+      const size_t xo = (size_t)s0 * r.dp;
 #pragma unroll
       for (int q = 0; q < D; q += 4) {
         float4 v;
@@ -480,7 +480,7 @@ __device__ __forceinline__ void pair_batch(const uint2* __restrict__ list, uint3
         nn = nn + v.y * v.y;
         nn = nn + v.z * v.z;
         nn = nn + v.w * v.w;
-        *reinterpret_cast<float4*>(xo + q) = v;
+        store_row4(r, xo + q, v);
       }
       r.nrm[s0] = nn;
       link_members(r, s1, s0);  // ids_current ++ ids_candidate; cnt[s1] = 0
@@ -1088,7 +1088,7 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
     for (int k = (int)t; k < d; k += NT) {
       const float v = consensus(xr[k], fa, ROWS_LDS ? lc[k] : xc[k], fb, fn);
       lc[k] = v;
-      if (!ROWS_LDS) xc[k] = v;  // rows in LDS go out once, at the end of the run
+      if (!ROWS_LDS) store_row1(r, (size_t)slot[c] * dp + k, v);  // LDS rows go out at the end
     }
     if (t == 0) {
       r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
@@ -1153,8 +1153,7 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
       const uint32_t q = idx / c4, k = (idx % c4) * 4;
       const uint32_t y = pos2row[q];
       if (r.cnt[slot[y]] != cnt[y])
-        *reinterpret_cast<float4*>(r.x + (size_t)slot[y] * dp + k) =
-            *reinterpret_cast<const float4*>(rowsL + y * ST + k);
+        store_row4(r, (size_t)slot[y] * dp + k, *reinterpret_cast<const float4*>(rowsL + y * ST + k));
     }
     __syncthreads();
   }
@@ -1420,8 +1419,7 @@ __device__ __forceinline__ void big_walk_reg(uint32_t p, uint32_t b, uint64_t* P
       const uint32_t q = idx / c4, k = (idx % c4) * 4;
       const uint32_t y = pos2row[q];
       if (r.cnt[slot[y]] != cnt[y])
-        *reinterpret_cast<float4*>(r.x + (size_t)slot[y] * r.dp + k) =
-            *reinterpret_cast<const float4*>(rowsL + y * ST + k);
+        store_row4(r, (size_t)slot[y] * r.dp + k, *reinterpret_cast<const float4*>(rowsL + y * ST + k));
     }
     __syncthreads();
   }
@@ -1819,7 +1817,7 @@ __device__ __forceinline__ void huge_runs(const uint2* __restrict__ list, uint32
         for (int k = (int)t; k < d; k += kHugeNT) {
           const float v = consensus(xa[k], fa, xj[k], fb, fn);
           xa[k] = v;  // the new row, for its norm
-          xj[k] = v;
+          store_row1(r, (size_t)sj * dp + k, v);
         }
         __syncthreads();  // the new row is in memory and in LDS
         if (t == 0) {
@@ -1876,7 +1874,7 @@ __device__ __forceinline__ void huge_runs(const uint2* __restrict__ list, uint32
         for (int k = (int)t; k < d; k += kHugeNT) {
           const float v = consensus(xi[k], fa, xj[k], fb, fn);
           xi[k] = v;  // the new row, for its norm
-          xj[k] = v;
+          store_row1(r, (size_t)sj * dp + k, v);
         }
         __syncthreads();  // the new row is in memory and in LDS
         if (t == 0) {
@@ -2099,7 +2097,8 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
       const float fa = (float)(int)ca, fb = (float)(int)cb, fn = (float)(int)(ca + cb);
       const float* xr = r.x + (size_t)slot_r * dp;
       float* xc = r.x + (size_t)slot_c * dp;
-      for (int k = (int)g; k < d; k += G) xc[k] = consensus(xr[k], fa, xc[k], fb, fn);
+      for (int k = (int)g; k < d; k += G)
+        store_row1(r, (size_t)slot_c * dp + k, consensus(xr[k], fa, xc[k], fb, fn));
       lds_fence();  // the new row c is visible to the group's lanes
       if (g == rr) alive = false;
       if (g == 0) r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)

@@ -274,7 +274,12 @@ __global__ __launch_bounds__(256) void k_delta_apply(Rows r, const uint32_t* __r
     case 2: r.head[s] = v; break;
     case 3: r.tail[s] = v; break;
     case 4: r.nrm[s] = __uint_as_float(v); break;
-    default: r.x[(size_t)s * r.dp + (w - 5)] = __uint_as_float(v);
+    default:
+      r.x[(size_t)s * r.dp + (w - 5)] = __uint_as_float(v);
+      if (r.xh) {  // the fp16 image of the replica's row follows it
+        const _Float16 hv = (_Float16)__uint_as_float(v);
+        r.xh[(size_t)s * r.dp + (w - 5)] = *reinterpret_cast<const uint16_t*>(&hv);
+      }
   }
   }
 }

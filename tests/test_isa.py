@@ -37,13 +37,17 @@ def test_target_is_gfx950(kernels):
 def test_projection_has_no_fused_multiply_add(kernels):
     proj = {k: v for k, v in kernels.items() if "k_project" in k}
     # d = 8, 16, 32, 64: packed (8 chains, 1 row per lane); the packed wide-row kernel; the generic
-    # kernel; the matrix-core kernels (d = 16, 32, 64; wide rows + their exact fix-up kernel)
-    assert len(proj) == 11
+    # kernel; the matrix-core kernels (d = 16, 32, 64; wide rows + their exact fix-up kernel);
+    # the fp16-image screens (d = 16, 32, 64; their close calls settled in the same kernel)
+    assert len(proj) == 14
     for name, body in proj.items():
         bad = [ln.strip() for ln in body.splitlines() if FMA.match(ln)]
         assert not bad, (name, bad[:5])
         if "mfma" in name:  # bf16x3 MFMA screen + the exact unfused chain for the close calls
             assert "v_mfma_f32_32x32x16_bf16" in body, name
+            assert "v_mul_f32" in body and "v_add_f32" in body, name
+        elif "h16" in name:  # fp16-image screen (x~ . (w_hi + w_lo)) + the exact unfused chain
+            assert "v_mfma_f32_32x32x16_f16" in body, name
             assert "v_mul_f32" in body and "v_add_f32" in body, name
         elif "_pk" in name:  # packed kernels: every product a separately rounded v_pk_mul_f32
             assert body.count("v_pk_mul_f32") == body.count("v_pk_add_f32") > 0, name
