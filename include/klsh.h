@@ -55,7 +55,8 @@ typedef struct klsh_ctx klsh_ctx;
 #define KLSH_K_TAIL 9     /* iterations below 2^20 positions: every merge class in one k_merge_tail */
 #define KLSH_K_COMPACT 10 /* survivor compaction (span) */
 #define KLSH_K_PAIRS 11   /* runs of 2 rows when they have a launch of their own (else in SMALL) */
-#define KLSH_KCLASSES 12
+#define KLSH_K_SCREEN 12  /* fp16 screen of the runs of 2..64 rows (SMALL then merges the ones left) */
+#define KLSH_KCLASSES 13
 typedef struct klsh_kstat {
   double ms;
   uint64_t launches;

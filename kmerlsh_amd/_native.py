@@ -41,8 +41,8 @@ EXPORTED = (
 
 # klsh_stats.kern indices (include/klsh.h KLSH_K_*)
 KERNEL_CLASSES = ("project", "sort", "runs", "small", "big128", "big192", "big384", "big896",
-                  "huge", "tail", "compact", "pairs")
-KCLASSES = 12
+                  "huge", "tail", "compact", "pairs", "screen")
+KCLASSES = 13
 
 
 class KlshKstat(ctypes.Structure):

@@ -268,6 +268,7 @@ struct klsh_ctx {
     pw.cap = 0;
     for (auto& c : mw.big) dfree(c);
     for (auto& c : mw.cls) dfree(c);
+    for (auto& c : mw.act) dfree(c);
     dfree(kstamp);
     dfree(lb.status);
     dfree(xh_alloc);
@@ -351,7 +352,8 @@ struct klsh_ctx {
       }
     }
     for (int c = 0; c < klsh::kGroupClasses; ++c) {
-      if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s)))) {
+      if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s))) ||
+          (e = dalloc(&mw.act[c], klsh::group_class_capacity(c, s)))) {
         release_state();
         return e;
       }
@@ -533,8 +535,14 @@ static void count_class_rows(klsh_stats* st, const Counters& c, uint64_t n, bool
     st->kern[KC_TAIL].runs += small_runs + big_runs;
     return;
   }
-  st->kern[KC_SMALL].rows += c.n_small_rows;
-  st->kern[KC_SMALL].runs += small_runs;
+  if (c.screened) {  // the screen saw every small run, the merge only the ones it passed
+    st->kern[KC_SCREEN].rows += c.n_small_rows;
+    st->kern[KC_SCREEN].runs += small_runs;
+    st->kern[KC_SMALL].rows += c.n_act_rows;
+  } else {
+    st->kern[KC_SMALL].rows += c.n_small_rows;
+    st->kern[KC_SMALL].runs += small_runs;
+  }
   for (int b = 0; b < kBigClasses; ++b) {
     st->kern[KC_BIG128 + b].rows += c.n_big_rows[b];
     st->kern[KC_BIG128 + b].runs += c.n_big[b];
@@ -889,7 +897,7 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
     KLSH_HIP(hipEventSynchronize(ctx->sev[1]));
     st->small_ms += elapsed(ctx->sev[0], ctx->sev[1]);
     st->small_launches += 1;
-    st->small_rows += ctx->h_ctr->n_small_rows;
+    st->small_rows += ctx->h_ctr->screened ? ctx->h_ctr->n_act_rows : ctx->h_ctr->n_small_rows;
     st->small_iter_merges += n - ctx->h_ctr->total;
   }
   if (timed && zc) KLSH_HIP(hipEventSynchronize(ctx->ev[4]));

@@ -51,6 +51,9 @@ struct alignas(128) CountLine {
 struct RunCounters {
   CountLine n_seg, n_cls[kGroupClasses], n_big[kBigClasses], n_huge, n_over, n_small_rows;
   CountLine n_big_rows[kBigClasses], n_huge_rows;  // rows in the big / huge runs (kernel rooflines)
+  // the small-run screen (k_small_screen): runs of each class it could not rule out, their rows,
+  // and a flag that it ran this iteration
+  CountLine n_act[kGroupClasses], n_act_rows, screened;
 };
 
 // Run-finding workspace (u32 words) for `slots` positions: 19 counts + a tail end + a 4096-bit
@@ -70,6 +73,8 @@ struct Counters {
   uint32_t n_small_rows;           // rows in the runs of 2..64 rows (the small-run merge's rows)
   uint32_t n_big_rows[kBigClasses];  // rows in the runs of each big class
   uint32_t n_huge_rows;            // rows in the runs of k_merge_huge
+  uint32_t n_act_rows;             // rows in the small runs the screen passed to k_merge_small
+  uint32_t screened;               // 1: the small-run screen ran this iteration
 };
 
 // Per-kernel-class timing (bench.py's roofline) from in-kernel stamps: every workgroup of a timed
@@ -84,7 +89,7 @@ struct Counters {
 // order) and clears it; the engine folds the last set at the end of a call.
 enum KClass : int {
   KC_PROJECT = 0, KC_SORT, KC_RUNS, KC_SMALL, KC_BIG128, KC_BIG192, KC_BIG384, KC_BIG896, KC_HUGE,
-  KC_TAIL, KC_COMPACT, KC_PAIRS, KC_COUNT
+  KC_TAIL, KC_COMPACT, KC_PAIRS, KC_SCREEN, KC_COUNT
 };
 constexpr int kStampSlots = 16;
 struct alignas(128) StampLine {
@@ -113,6 +118,10 @@ constexpr KTime kNoTime{nullptr, 0, -1};
 // Merge workspace (device), sized for `cap` positions.
 struct MergeWork {
   uint2* cls[kGroupClasses];       // (start, length) of runs per size class
+  // the runs of each class the fp16 screen could not rule out (k_small_screen), and whether the
+  // small-run merge reads these instead of cls (set per launch)
+  uint2* act[kGroupClasses];
+  uint32_t screened;
   uint2* big[kBigClasses];         // (start, length) of runs for k_merge_big, per class
   uint2* huge;                     // (start, length) of runs for k_merge_huge
   uint2* over;                     // (start, length) of oversize runs
