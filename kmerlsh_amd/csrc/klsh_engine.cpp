@@ -971,8 +971,10 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
     return e;
   // many 385..896-row runs this iteration: the next one runs that class on an auxiliary stream
   ctx->mw.big896_aux = ctx->h_ctr->n_big[klsh::kBigClasses - 1] >= 64u ? 1u : 0u;
-  // no >896-row runs this iteration: the next one's launch for them is 4 workgroups
-  ctx->mw.huge_cap = ctx->h_ctr->n_huge == 0 ? 4u : 0u;
+  // no >896-row runs this iteration: the next one's launch for them is 64 workgroups (C4 has
+  // iterations without them between ones with dozens: a cap of 4 serialised those walks,
+  // k_merge_huge<32> 746 -> 1024 ms per step)
+  ctx->mw.huge_cap = ctx->h_ctr->n_huge == 0 ? 64u : 0u;
   if (ctx->h_ctr->n_over > 0) {
     std::vector<uint2> over;
     uint64_t hyp = 0;

@@ -141,8 +141,8 @@ struct MergeWork {
   // the engine when the previous iteration had many of them (C4: thousands; C2: < 10)
   uint32_t big896_aux;
   // >896-row runs: the launch's workgroup cap (0 = one per 897 positions, at most 512).  The
-  // engine sets a small cap after an iteration without such runs: an empty launch of hundreds of
-  // 512-lane workgroups waits for CUs behind the other classes (C2: 25 ms per step for no runs)
+  // engine sets a cap of 64 after an iteration without such runs: an empty launch of hundreds of
+  // 512-lane workgroups waits for CUs behind the other classes (C2: 25 ms per step of span)
   uint32_t huge_cap;
   hipStream_t aux[3];
   KTime kt;                // per-class stamps of this iteration's merge launches
