@@ -2644,7 +2644,11 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   if (screen_ok(r, dc)) {
     float m0, a2;
     screen_margins(r.d, &m0, &a2);
-    k_small_screen<D><<<8192, 64, 0, f.lane(2)>>>(w, slots, r, dc.s_star, m0, a2, w.kt);
+    static const uint32_t sgrid = [] {  // (KLSH_SCREEN_GRID: A/B of the launch size)
+      const char* e = getenv("KLSH_SCREEN_GRID");
+      return e ? (uint32_t)std::max(64, atoi(e)) : 2048u;  // 512..4096 swept: 2048 best
+    }();
+    k_small_screen<D><<<sgrid, 64, 0, f.lane(2)>>>(w, slots, r, dc.s_star, m0, a2, w.kt);
     MergeWork ws = w;
     ws.screened = 1u;
     if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
