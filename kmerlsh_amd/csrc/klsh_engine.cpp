@@ -177,6 +177,7 @@ struct klsh_ctx {
   bool spec_pending = false;
   uint64_t spec_k = 0;
   int spec_ev = 0;
+  bool spec_swap = false;  // the queued keys went to keys2 (this iteration's sorted keys were in keys)
   bool zero_copy = true;
   klsh::RunCounters* rc = nullptr;  // run-list counters (device, one 128-B line each)
   // fp16 image of the rows for the projection's screen (Rows::xh; KLSH_SHADOW=0: off); every row
@@ -1032,6 +1033,8 @@ static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, 
   KLSH_HIP(hipMemsetD32Async(woff_dev, (int)(uint32_t)(k0 - ctx->w_k0), 1, s));
   bool queued = ctx->spec_pending;  // the first projection is already on the stream
   ctx->spec_pending = false;
+  if (queued && ctx->spec_swap) std::swap(ctx->keys, ctx->keys2);
+  ctx->spec_swap = false;
   if (!queued && !ctx->ctr_clean)
     if (int e = ctx->reset_counters()) return e;
   if (queued && ctx->spec_k != k0) return fail(KLSH_E_STATE, "queued projection out of step");
@@ -1153,6 +1156,8 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     // the projection: queued by the previous iteration (device-side N), or now
     const bool queued = ctx->spec_pending;
     ctx->spec_pending = false;
+    if (queued && ctx->spec_swap) std::swap(ctx->keys, ctx->keys2);  // the queued keys' buffer
+    ctx->spec_swap = false;
     const uint64_t j = ctx->kt_iter++;  // this iteration's stamp set
     if (queued && ctx->spec_k != k) return fail(KLSH_E_STATE, "queued projection out of step");
     const int e0 = queued ? ctx->spec_ev : 0;
@@ -1201,23 +1206,24 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     }
     // Queue the next iteration's projection behind this compaction.  If this iteration turns out
     // to have oversize buckets (nestedCluster changes rows and draws hyperplanes first), the
-    // queued keys are simply recomputed; they go to ctx->keys, which the nested work must not be
-    // reading — so only when the sorted keys of this iteration are in the other buffer.
+    // queued keys are simply recomputed; they go to the key buffer the nested work is not reading
+    // (this iteration's sorted keys fk stay intact), keys2 when fk is keys — the next iteration
+    // then swaps the two pointers.
     const bool ahead = ctx->zero_copy && it + 1 < it_end &&
-                       klsh::project_device_n_ok(ctx->d) && !getenv("KLSH_BUCKET_STATS") &&
-                       (fk != ctx->keys || (bucket_size_threshold >= 0 &&
-                                            n <= (uint64_t)bucket_size_threshold));
+                       klsh::project_device_n_ok(ctx->d) && !getenv("KLSH_BUCKET_STATS");
+    uint32_t* const spec_out = fk == ctx->keys ? ctx->keys2 : ctx->keys;
     const std::function<int(uint32_t*)> queue_next = [&](uint32_t* next_order) -> int {
       const uint64_t k_next = k + (uint64_t)h;  // h_next <= h: inside the drawn window
       if (int e = ctx->ensure_hyperplanes(seed_base, k_next, (uint64_t)h, &st->host_ms)) return e;
       const int ne = e0 == 0 ? 6 : 0;
       if (rec) KLSH_HIP(hipEventRecord(ctx->ev[ne], s));
-      klsh::launch_project_device_n(ctx->rows, next_order, ctx->keys, (uint32_t)n,
+      klsh::launch_project_device_n(ctx->rows, next_order, spec_out, (uint32_t)n,
                                     ctx->hyperplane_ptr(k_next), ctx->n_next_dev, s, ktime(j + 1),
                                     nullptr, &ctx->pw);
       KLSH_HIP(hipGetLastError());
       if (rec) KLSH_HIP(hipEventRecord(ctx->ev[ne + 1], s));
       ctx->spec_pending = true;
+      ctx->spec_swap = spec_out == ctx->keys2;
       ctx->spec_k = k_next;
       ctx->spec_ev = ne;
       return 0;
@@ -1226,7 +1232,10 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
                                   seed_base, rng_counter, st, ctx->phase_timing,
                                   ahead ? &queue_next : nullptr, ktime(j)))
       return e;
-    if (ctx->spec_pending && *rng_counter != ctx->spec_k) ctx->spec_pending = false;  // nested ran
+    if (ctx->spec_pending && *rng_counter != ctx->spec_k) {  // nested ran: recomputed next time
+      ctx->spec_pending = false;
+      ctx->spec_swap = false;
+    }
     if (rec) st->project_ms += elapsed(ctx->ev[e0], ctx->ev[e0 + 1]);
     if (rec && ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
     st->project_launches += 1;
@@ -1547,6 +1556,7 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
 
   ctx->ctr_clean = false;
   ctx->spec_pending = false;
+  ctx->spec_swap = false;
   // no run counts yet: only very large inputs start with the 385..896-row class on aux 2
   ctx->mw.big896_aux = ctx->n_live >= (1u << 24) ? 1u : 0u;
   // Every call draws its hyperplanes afresh (the reference draws them inside Cluster(),
