@@ -201,7 +201,9 @@ struct ProjectWork {
   uint32_t* ws;
   uint32_t cap;
 };
-constexpr uint32_t kH16Grid = 8192;  // workgroups of the fp16-image screen, at most
+// workgroups of the fp16-image projection, at most (C2 per step: 2048 -> 46.1, 4096 -> 46.5,
+// 8192 -> 48.5, 16384 -> 52.9, 32768 -> 55.5 ms, interleaved on one box)
+constexpr uint32_t kH16Grid = 2048;
 
 // ---- launch wrappers (all asynchronous on `s`) ------------------------------------------------
 // keys[p] = sign-hash of row slots[p] against h hyperplanes W (h x dp), OR'ed with key_or.

@@ -845,7 +845,11 @@ static void launch_h16(const Rows& r, const uint32_t* slots, uint32_t* keys, uin
                        const float* W, int h, uint32_t key_or, hipStream_t s,
                        const ProjectWork& pw, KTime kt, const uint32_t* n_dev,
                        const uint32_t* woff_dev) {
-  const uint32_t grid = std::min<uint32_t>((n + 255) / 256, kH16Grid);
+  static const uint32_t gmax = [] {  // (KLSH_H16_GRID: A/B of the launch size)
+    const char* e = getenv("KLSH_H16_GRID");
+    return e ? (uint32_t)std::max(256, atoi(e)) : kH16Grid;
+  }();
+  const uint32_t grid = std::min<uint32_t>((n + 255) / 256, gmax);
   const uint32_t segcap = (pw.cap / 2) / grid;  // 16-B fix-up entries per workgroup
   const float eps = h16_eps(r.d), abs_c = h16_abs(r.d);
   auto go = [&](auto screen) {
