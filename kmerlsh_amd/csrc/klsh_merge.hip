@@ -2609,7 +2609,14 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_tail<D>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
     (void)lds_ok;
-    const uint32_t nbig = 64, nsmall = 256;
+    static const uint32_t nbig = [] {  // (KLSH_TAIL_NBIG / KLSH_TAIL_NSMALL: A/B of the split)
+      const char* e = getenv("KLSH_TAIL_NBIG");
+      return e ? (uint32_t)std::max(1, atoi(e)) : 128u;  // 32 / 64 / 128 / 256 swept
+    }();
+    static const uint32_t nsmall = [] {
+      const char* e = getenv("KLSH_TAIL_NSMALL");
+      return e ? (uint32_t)std::max(1, atoi(e)) : 512u;  // 128 / 256 / 512 / 1024 swept
+    }();
     k_merge_tail<D><<<nbig + nsmall, 256, lds, s>>>(w, slots, dc, r, ctr, nbig);
     return;
   }
