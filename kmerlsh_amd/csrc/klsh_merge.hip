@@ -2590,6 +2590,15 @@ static bool screen_ok(const Rows& r, const Decider& dc) {
   return on && r.xh && dc.fast && (r.d == 32 || r.d == 64);  // (16x16x32 tiles: d >= 32)
 }
 
+// The small-run merge's persistent launch (KLSH_SMALL_GRID: A/B of its size; default 12288).
+static uint32_t small_grid() {
+  static const uint32_t g = [] {
+    const char* e = getenv("KLSH_SMALL_GRID");
+    return e ? (uint32_t)std::max(256, atoi(e)) : 12288u;
+  }();
+  return g;
+}
+
 // Iterations below this many positions run every merge class in ONE launch (k_merge_tail) on the
 // main stream: there the cross-stream fork/join (~35 us) costs more than the overlap buys.
 constexpr uint32_t kTailMergeMax = 1u << 20;
@@ -2659,10 +2668,10 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
     MergeWork ws = w;
     ws.screened = 1u;
     if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
-    k_merge_small<D><<<12288, 64, 0, f.lane(2)>>>(ws, slots, dc, r, ctr);
+    k_merge_small<D><<<small_grid(), 64, 0, f.lane(2)>>>(ws, slots, dc, r, ctr);
   } else {
     if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
-    k_merge_small<D><<<12288, 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
+    k_merge_small<D><<<small_grid(), 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
   }
   if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[1], f.lane(2));
 }
