@@ -919,7 +919,14 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
                               hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) == hipSuccess;
       (void)lds_ok;
       const uint32_t groups = (n + kWideNT / 2 - 1) / (kWideNT / 2);  // 32 rows per wave
-      const dim3 gm(std::min<uint32_t>(groups, 2048u));
+      static const uint32_t wcap = [] {  // (KLSH_WIDE_GRID: A/B of the launch size)
+        const char* e = getenv("KLSH_WIDE_GRID");
+        // one resident round (2 workgroups of 6 waves per CU): C5 projection 1203 -> 1076 ms per
+        // step (256..8192 swept on one box: 256 -> 1073, 512 -> 1076, 1024 -> 1112, 2048 -> 1203,
+        // 4096 -> 1318, 8192 -> 1533)
+        return e ? (uint32_t)std::max(64, atoi(e)) : 512u;
+      }();
+      const dim3 gm(std::min<uint32_t>(groups, wcap));
       // stamped as one span: the screen (start) and the fix-up of its close calls (end)
       KTime k1 = kt;
       k1.fold = -1;
