@@ -932,7 +932,11 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
       k1.fold = -1;
       k_project_mfma_wide<<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h,
                                                          key_or, project_eps(r.d), *pw, kt);
-      k_project_fix<<<1024, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
+      static const uint32_t fcap = [] {  // (KLSH_FIX_GRID: A/B of the fix-up launch size)
+        const char* e = getenv("KLSH_FIX_GRID");
+        return e ? (uint32_t)std::max(16, atoi(e)) : 1024u;
+      }();
+      k_project_fix<<<fcap, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
       return;
     }
   }
