@@ -2697,7 +2697,11 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
   auto grid = [&](int c, uint32_t per_wave) {
     // up to 8192 one-wave workgroups per class (was 2048: C5 2.58 / 2.55 -> 2.36 / 2.33 s per
     // step, interleaved on one box), as for the register-row small-run launch
-    return (uint32_t)std::min<uint64_t>(8192, group_class_capacity(c, n) / per_wave + 1);
+    static const uint64_t cap = [] {  // (KLSH_WIDE_GROUP_GRID: A/B of the launch size)
+      const char* e = getenv("KLSH_WIDE_GROUP_GRID");
+      return e ? (uint64_t)std::max(64, atoi(e)) : 8192ull;
+    }();
+    return (uint32_t)std::min<uint64_t>(cap, group_class_capacity(c, n) / per_wave + 1);
   };
   const Fork f(w, s);
   launch_big_wide<384, 256, 32>(w, 2, slots, dc, r, ctr, n, f.lane(0));
