@@ -2699,7 +2699,8 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
     // step, interleaved on one box), as for the register-row small-run launch
     static const uint64_t cap = [] {  // (KLSH_WIDE_GROUP_GRID: A/B of the launch size)
       const char* e = getenv("KLSH_WIDE_GROUP_GRID");
-      return e ? (uint64_t)std::max(64, atoi(e)) : 8192ull;
+      // 4096 -> 1221, 8192 -> 1141, 16384 -> 1103, 32768 -> 1102 ms per C5 step (one box)
+      return e ? (uint64_t)std::max(64, atoi(e)) : 16384ull;
     }();
     return (uint32_t)std::min<uint64_t>(cap, group_class_capacity(c, n) / per_wave + 1);
   };
