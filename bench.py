@@ -279,9 +279,7 @@ def pmc_traffic(config, kernel):
 #   project   rows x (4d row + 4 slot + 4 key)
 #   sort      sum over iterations of N_t x passes_t x 20 (hist: key; scatter: key + slot in and out)
 #   runs      rows x 4 (sorted keys) + runs x 8 (list entries)
-#   small     rows x (4d + 4) (row + slot) + merges x (4d + 20) (new row, norm, count, head, link);
-#             after the screen, its rows are those of the runs the screen passed
-#   screen    rows x (2d + 4) (fp16 row + slot) + runs x 8 (list entries)
+#   small     rows x (4d + 4) (row + slot) + merges x (4d + 20) (new row, norm, count, head, link)
 #   big*/huge rows x (4d + 20) (row, slot, count, head, tail, the slot written back)
 #   tail      rows x (4d + 8) (all merge classes of a small iteration in one launch)
 #   compact   rows x 12 (slots read twice, survivors written)
@@ -291,8 +289,7 @@ KERNEL_NAMES = {
     "big128": "k_merge_big<{d},128,128,true>", "big192": "k_merge_big<{d},192,256,true>",
     "big384": "k_merge_big<{d},384,256,true>", "big896": "k_merge_big<{d},896,256,false>",
     "huge": "k_merge_huge<{d}>", "tail": "k_merge_tail<{d}>",
-    "compact": "k_compact_count/apply (span)", "pairs": "k_merge_pairs<{d}>",
-    "screen": "k_small_screen<{d}>",
+    "compact": "k_compact_count/apply (span)",
 }
 WIDE_NAMES = {
     "project": "k_project_mfma_wide + k_project_fix (span)",
@@ -304,15 +301,14 @@ WIDE_NAMES = {
 BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
-def kernel_rooflines(config, stats, steps, d, trace):
+def kernel_rooflines(config, stats, steps, d, trace, shadow):
     """Every kernel class's achieved HBM rate (its algorithmic bytes per launch over its average
     HIP-event launch time); the headline is the class with the largest time per step."""
     import math
 
     register = d in (8, 16, 32, 64)
-    # the projection reads the fp16 row image (2d bytes a row) where the engine keeps one
-    # (d = 16, 32, 64; KLSH_SHADOW=0 turns it off); its close calls re-read the f32 row (k_project_fix)
-    shadow = d in (16, 32, 64) and os.environ.get("KLSH_SHADOW", "1") != "0"
+    # shadow: the projection reads the fp16 row image (2d bytes a row; the engine keeps one at
+    # d = 16, 32, 64 unless option "projection" = 1); its close calls re-read the f32 row
     row_bytes = 2 * d if shadow else 4 * d
     kern = {c: {f: sum(s["kern"][c][f] for s in stats) for f in ("ms", "launches", "rows", "runs")}
             for c in stats[0]["kern"]}
@@ -327,7 +323,6 @@ def kernel_rooflines(config, stats, steps, d, trace):
             continue
         rows, runs = k["rows"], k["runs"]
         b = {"project": rows * (row_bytes + 8), "sort": sort_bytes, "runs": rows * 4 + runs * 8,
-             "screen": rows * (2 * d + 4) + runs * 8,
              "small": rows * (4 * d + 4) + merges_small * (4 * d + 20),
              "tail": rows * (4 * d + 8), "compact": rows * 12}.get(c, rows * (4 * d + 20))
         avg = k["ms"] / k["launches"]
@@ -349,7 +344,7 @@ def kernel_rooflines(config, stats, steps, d, trace):
         # shares the CUs with them and an event pair would include its waits for resources)
         ev_ms = {"project": sum(s["project_ms"] for s in stats),
                  "small": sum(s["small_ms"] for s in stats)}.get(c)
-        ev_n = {"project": sum(s["project_launches"] for s in stats),
+        ev_n = {"project": sum(s["project_timed_launches"] for s in stats),
                 "small": sum(s["small_launches"] for s in stats)}.get(c)
         e["timing"] = "stamps"
         if ev_ms and ev_n:
@@ -426,8 +421,6 @@ def main():
                     help="profiling only: override the config's -I (the metric is then not C2's)")
     args = ap.parse_args()
 
-    if args.phases:
-        os.environ["KLSH_PHASE_TIMING"] = "1"
     world, rank, local = dist_setup()
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
@@ -438,6 +431,8 @@ def main():
     from kmerlsh_amd import _native
 
     eng = _native.Engine(local)
+    if args.phases:
+        eng.set_option("phase_timing", 1)
     sharded = world > 1 and args.mode == "sharded"
     if sharded:
         import torch.distributed as dist
@@ -478,7 +473,8 @@ def main():
     # rows x (4d row + 4 slot) + merges x (4d new row + 20 metadata: norm, count, head, member
     # link, the removed row's count) — merges counted over the whole iteration (~97 % of them are
     # small-run merges on C2).  The bench line's "roofline" is the one with the larger time per step.
-    roofline = kernel_rooflines(args.config, stats, args.steps, d, trace)
+    roofline = kernel_rooflines(args.config, stats, args.steps, d, trace,
+                                bool(eng.get_option("fp16_image")))
     # the whole loop against HBM, SURVEY.md §8(d): B_t = N_t (8d + 16) + M_t (4d + 8) bytes per
     # iteration (rows read by the projection and by the merge, keys and order written and read;
     # per merge the new row and a member link), summed over the timed steps

@@ -37,6 +37,11 @@ extern "C" {
 #define KLSH_E_NODEVICE (-5) /* no gfx950 device visible: the engine has no CPU fallback */
 #define KLSH_E_RANGE (-6)    /* a size exceeds what the engine supports (rows >= 2^32, d > 4096) */
 
+/* ABI version of this header.  2: every statistics struct starts with `struct_size`, which the
+ * caller sets to sizeof(the struct) (the library refuses a mismatch instead of writing past a
+ * smaller struct); klsh_stats.kern has KLSH_KCLASSES = 11 classes; klsh_get_option. */
+#define KLSH_ABI_VERSION 2
+
 typedef struct klsh_ctx klsh_ctx;
 
 /* Per-kernel-class statistics of a call: summed span of the class's launches (first workgroup
@@ -54,9 +59,7 @@ typedef struct klsh_ctx klsh_ctx;
 #define KLSH_K_HUGE 8     /* longer runs (k_merge_huge) */
 #define KLSH_K_TAIL 9     /* iterations below 2^20 positions: every merge class in one k_merge_tail */
 #define KLSH_K_COMPACT 10 /* survivor compaction (span) */
-#define KLSH_K_PAIRS 11   /* runs of 2 rows when they have a launch of their own (else in SMALL) */
-#define KLSH_K_SCREEN 12  /* fp16 screen of the runs of 2..64 rows (SMALL then merges the ones left) */
-#define KLSH_KCLASSES 13
+#define KLSH_KCLASSES 11
 typedef struct klsh_kstat {
   double ms;
   uint64_t launches;
@@ -66,6 +69,7 @@ typedef struct klsh_kstat {
 
 /* Per-call statistics (all times are milliseconds). */
 typedef struct klsh_stats {
+  uint64_t struct_size;    /* in: sizeof(klsh_stats) (KLSH_ABI_VERSION check) */
   uint64_t iterations;     /* iterations run */
   uint64_t sum_rows;       /* sum over iterations of N_t (rows projected) */
   uint64_t sum_merges;     /* sum over iterations of M_t = N_t - N_{t+1} */
@@ -73,9 +77,11 @@ typedef struct klsh_stats {
   uint64_t nested_calls;   /* oversize buckets sent through nestedCluster */
   uint64_t hyperplanes;    /* hyperplanes drawn by this call */
   uint64_t n_final;        /* live rows after the call */
-  uint64_t project_launches;
+  uint64_t project_launches;        /* projection launches (every iteration has one) */
+  uint64_t project_timed_launches;  /* the ones inside project_ms (queued tail batches carry no
+                                       HIP events; their time is in kern[KLSH_K_PROJECT]) */
   double wall_ms;          /* host wall clock of the whole call */
-  double project_ms;       /* HIP-event time of the projection kernel launches */
+  double project_ms;       /* HIP-event time of project_timed_launches projection launches */
   double sort_ms;          /* HIP-event time of the bucket (radix) sort */
   double merge_ms;         /* HIP-event time of the greedy in-bucket merge kernels */
   double compact_ms;       /* HIP-event time of the survivor compaction */
@@ -102,6 +108,7 @@ klsh_ctx* klsh_create(int device, int* err);
 void klsh_destroy(klsh_ctx* ctx);
 const char* klsh_last_error(void);  /* thread-local text for the last failure */
 const char* klsh_version(void);
+int klsh_abi_version(void);         /* KLSH_ABI_VERSION of the built library */
 
 /* ---- loading the rows (replaces building vector<Abundance*>) ---------------------------------- */
 /* rows: n x d fp32 row-major (reference common/abundance.h:18-36, `_values`).
@@ -143,14 +150,30 @@ int klsh_comm_init(klsh_ctx* ctx, int rank, int world, const uint8_t* id /* 128 
  * klsh_cluster must then run on its own host thread, concurrently.  For tests on one GPU. */
 int klsh_comm_init_local(klsh_ctx** ctxs, int world);
 int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
-/* Options: "shard_min_rows" (sharded loop: below this many live rows every rank runs the
- * remaining iterations on its own replica, without exchanges; default 2097152 = 2^21, 0 = always
- * sharded), "phase_timing" (0/1: per-phase HIP events, adds latency), "kernel_timing" (0/1,
- * default 1: the per-class statistics of klsh_stats.kern) — results never depend on them; "stop_after" (k > 0: klsh_cluster runs only the first k iterations of its threshold
- * schedule, e.g. to pin a prefix of a long loop; 0 = all, the default), "hyperplane_window"
- * (hyperplane rows drawn up front per call; the rest are drawn when the loop reaches them; 0 =
- * the default: all of them while they fit in 256 MB, else 64 iterations' worth). */
+/* Options of a context.  Results never depend on them, except "stop_after".
+ *   "shard_min_rows"   sharded loop: below this many live rows every rank runs the remaining
+ *                      iterations on its own replica, without exchanges (default 2^21; 0 = always)
+ *   "phase_timing"     0/1: per-phase HIP events (adds latency; default 0)
+ *   "kernel_timing"    0/1: the per-class statistics of klsh_stats.kern (default 1)
+ *   "tail_batch"       0/1: queue the small late iterations 32 at a time (default 1)
+ *   "projection"       0 = the certified matrix-core screens where they exist (default: the fp16
+ *                      row image at d = 16, 32, 64 — kept beside the rows, 2 bytes per value —
+ *                      and bf16x3 above 64), 1 = the exact packed VALU chains only (no fp16 image)
+ *   "stop_after"       k > 0: klsh_cluster runs only the first k iterations of its threshold
+ *                      schedule, e.g. to pin a prefix of a long loop; 0 = all (default)
+ *   "hyperplane_window" hyperplane rows drawn up front per call; the rest are drawn when the loop
+ *                      reaches them (0 = default: all of them while they fit in 256 MB, else 64
+ *                      iterations' worth)
+ *   "comm_timeout_s"   a collective still incomplete after this many seconds aborts (default 600)
+ *   launch sizes, 0 = the measured default: "h16_grid", "wide_grid", "fix_grid" (projection),
+ *   "small_grid", "tail_big_groups", "tail_small_groups", "wide_group_grid" (merge);
+ *   "h16_segcap" (tests) caps the fp16 projection's per-workgroup fix-up segment. */
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
+/* Any option above, plus read-only diagnostics: "fp16_image" (1 = the loaded rows have the fp16
+ * image), "last_hash_kernel" (klsh_hash_keys' projection kernel: 0 packed chains, 1 fp16-image
+ * screen, 2 bf16x3 wide-row screen, -1 none) and "last_hash_close_pairs" (its (row, hyperplane)
+ * pairs settled by the exact chains). */
+int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value);
 
 /* ---- results ---------------------------------------------------------------------------------- */
 int klsh_count(klsh_ctx* ctx, uint64_t* n_rows, uint64_t* n_members);
@@ -160,7 +183,9 @@ int klsh_result(klsh_ctx* ctx, float* rows, uint64_t* member_offsets, uint64_t* 
 
 /* ---- path functions, exposed for parity tests ------------------------------------------------- */
 /* Hash::LSH::random_projection(row, table) (reference hash/lshash.cc:44-59) for n rows on the
- * GPU: keys[i] = MSB-first sign bits of the h hyperplanes (table: h x d, row-major). */
+ * GPU: keys[i] = MSB-first sign bits of the h hyperplanes (table: h x d, row-major).  The same
+ * kernels and options as the loop's projection (the fp16 row image is built from `rows` where
+ * the loop would keep one). */
 int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const float* table, int h,
                    uint32_t* keys);
 /* merge_hashtable (reference function/cluster.cc:15-30) on the GPU: the stable bucket order of n
@@ -219,6 +244,7 @@ int klsh_check_reads(klsh_ctx* ctx, const klsh_kset* set, const char* seq,
                      const uint64_t* read_offsets, uint64_t n_reads, int k, float kmer_vote,
                      uint32_t* hits, uint8_t* flags);
 typedef struct klsh_extract_stats {
+  uint64_t struct_size; /* in: sizeof(klsh_extract_stats) */
   uint64_t reads, bases, reads_tested, kmers_checked, reads_extracted, abnormal;
   double kernel_ms;  /* HIP-event time of the k-mer vote kernels */
   double parse_ms;   /* host FASTQ parsing (gzip included) */
@@ -241,6 +267,7 @@ int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* set, const char* in_path,
  * as if those threads ran one after another).
  * out_dir NULL or "" = the current directory.  stats may be NULL. */
 typedef struct klsh_khtable_stats {
+  uint64_t struct_size; /* in: sizeof(klsh_khtable_stats) */
   uint64_t kmap_size, records, records_listed;
   double io_ms;     /* host reads of the .kmc_suf streams */
   double total_ms;

@@ -72,7 +72,8 @@ void Cluster(std::vector<Abundance*>* rows, float min_similarity, int cluster_it
   }
   check(klsh_load_rows(P.ctx, x.data(), n, dim, off.data(), ids.data()), "klsh_load_rows");
   std::vector<uint64_t> trace(cluster_iteration > 0 ? cluster_iteration : 1);
-  klsh_stats st;
+  klsh_stats st{};
+  st.struct_size = sizeof(st);
   check(klsh_cluster(P.ctx, min_similarity, cluster_iteration, bucket_size_threshold, P.seed,
                      &P.counter, trace.data(), &st),
         "klsh_cluster");

@@ -28,21 +28,24 @@ ERRORS = {
 
 # Every symbol include/klsh.h declares (tests/test_native_lib.py checks the .so exports them).
 EXPORTED = (
-    "klsh_create", "klsh_destroy", "klsh_last_error", "klsh_version", "klsh_load_rows",
+    "klsh_create", "klsh_destroy", "klsh_last_error", "klsh_version", "klsh_abi_version",
+    "klsh_load_rows",
     "klsh_load_counts", "klsh_snapshot", "klsh_restore", "klsh_cluster", "klsh_count",
     "klsh_result", "klsh_hash_keys", "klsh_bucket_sort", "klsh_pcluster", "klsh_hyperplanes", "klsh_fp_selftest",
     "klsh_synth_counts", "klsh_comm_unique_id", "klsh_comm_init", "klsh_comm_init_local",
-    "klsh_comm_info", "klsh_set_option", "klsh_wrs", "klsh_ttest2", "klsh_fastq_open",
+    "klsh_comm_info", "klsh_set_option", "klsh_get_option", "klsh_wrs", "klsh_ttest2", "klsh_fastq_open",
     "klsh_fastq_next", "klsh_fastq_close", "klsh_kset_create", "klsh_kset_destroy",
     "klsh_check_reads", "klsh_extract_fastq", "klsh_build_khtable", "klsh_cuckoo_order",
     "klsh_kmc_info",
 )
 
 
+# include/klsh.h KLSH_ABI_VERSION (the structs below mirror that header)
+ABI_VERSION = 2
 # klsh_stats.kern indices (include/klsh.h KLSH_K_*)
 KERNEL_CLASSES = ("project", "sort", "runs", "small", "big128", "big192", "big384", "big896",
-                  "huge", "tail", "compact", "pairs", "screen")
-KCLASSES = 13
+                  "huge", "tail", "compact")
+KCLASSES = 11
 
 
 class KlshKstat(ctypes.Structure):
@@ -54,8 +57,20 @@ class KlshKstat(ctypes.Structure):
     ]
 
 
-class KlshStats(ctypes.Structure):
+class _Sized(ctypes.Structure):
+    """A statistics struct whose leading struct_size field the caller fills in."""
+
+    def __init__(self):
+        super().__init__()
+        self.struct_size = ctypes.sizeof(self)
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "struct_size"}
+
+
+class KlshStats(_Sized):
     _fields_ = [
+        ("struct_size", ctypes.c_uint64),
         ("iterations", ctypes.c_uint64),
         ("sum_rows", ctypes.c_uint64),
         ("sum_merges", ctypes.c_uint64),
@@ -64,6 +79,7 @@ class KlshStats(ctypes.Structure):
         ("hyperplanes", ctypes.c_uint64),
         ("n_final", ctypes.c_uint64),
         ("project_launches", ctypes.c_uint64),
+        ("project_timed_launches", ctypes.c_uint64),
         ("wall_ms", ctypes.c_double),
         ("project_ms", ctypes.c_double),
         ("sort_ms", ctypes.c_double),
@@ -81,14 +97,15 @@ class KlshStats(ctypes.Structure):
     ]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "kern"}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("kern", "struct_size")}
         d["kern"] = {name: {f: getattr(self.kern[i], f) for f, _ in KlshKstat._fields_}
                      for i, name in enumerate(KERNEL_CLASSES)}
         return d
 
 
-class KlshExtractStats(ctypes.Structure):
+class KlshExtractStats(_Sized):
     _fields_ = [
+        ("struct_size", ctypes.c_uint64),
         ("reads", ctypes.c_uint64),
         ("bases", ctypes.c_uint64),
         ("reads_tested", ctypes.c_uint64),
@@ -100,12 +117,10 @@ class KlshExtractStats(ctypes.Structure):
         ("total_ms", ctypes.c_double),
     ]
 
-    def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
 
-
-class KlshKhtableStats(ctypes.Structure):
+class KlshKhtableStats(_Sized):
     _fields_ = [
+        ("struct_size", ctypes.c_uint64),
         ("kmap_size", ctypes.c_uint64),
         ("records", ctypes.c_uint64),
         ("records_listed", ctypes.c_uint64),
@@ -113,9 +128,6 @@ class KlshKhtableStats(ctypes.Structure):
         ("total_ms", ctypes.c_double),
         ("order_ms", ctypes.c_double),
     ]
-
-    def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class KlshError(RuntimeError):
@@ -144,6 +156,7 @@ def load_library() -> ctypes.CDLL:
         "klsh_destroy": (None, [_P]),
         "klsh_last_error": (ctypes.c_char_p, []),
         "klsh_version": (ctypes.c_char_p, []),
+        "klsh_abi_version": (ctypes.c_int, []),
         "klsh_load_rows": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, _P, _P]),
         "klsh_load_counts": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64,
                                             ctypes.c_uint64, ctypes.c_int, _P]),
@@ -168,6 +181,7 @@ def load_library() -> ctypes.CDLL:
         "klsh_comm_info": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int),
                                           ctypes.POINTER(ctypes.c_int)]),
         "klsh_set_option": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int64]),
+        "klsh_get_option": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
         "klsh_wrs": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _P,
                                     ctypes.c_float, ctypes.c_int, _P]),
         "klsh_ttest2": (ctypes.c_int, [_P, ctypes.c_int64, _P, ctypes.c_int64, _P, _P, _P]),
@@ -191,6 +205,9 @@ def load_library() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if not os.environ.get("KLSH_LIB") and lib.klsh_abi_version() != ABI_VERSION:
+        raise KlshError(f"{LIB_PATH}: ABI version {lib.klsh_abi_version()}, this binding "
+                        f"mirrors {ABI_VERSION}: rebuild the library")
     _lib = lib
     return lib
 
@@ -411,6 +428,12 @@ class Engine:
 
     def set_option(self, name: str, value: int) -> None:
         _check(self._lib.klsh_set_option(self._ctx, name.encode(), int(value)), "klsh_set_option")
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64(0)
+        _check(self._lib.klsh_get_option(self._ctx, name.encode(), ctypes.byref(v)),
+               "klsh_get_option")
+        return v.value
 
     def comm_info(self) -> tuple[int, int]:
         r = ctypes.c_int(0)

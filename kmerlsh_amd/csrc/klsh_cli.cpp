@@ -82,7 +82,8 @@ void fetch(klsh_ctx* ctx, int d, RowSet* out) {
 void run_cluster(klsh_ctx* ctx, float min_sim, int iters, int bthr, uint32_t seed,
                  uint64_t* counter, bool verbose) {
   std::vector<uint64_t> trace(iters > 0 ? iters : 1);
-  klsh_stats st;
+  klsh_stats st{};
+  st.struct_size = sizeof(st);
   check(klsh_cluster(ctx, min_sim, iters, bthr, seed, counter, trace.data(), &st), "klsh_cluster");
   if (verbose) {
     for (uint64_t t = 0; t < st.iterations; ++t)
@@ -149,7 +150,8 @@ int run_build(klsh_ctx* ctx, const char* in1, const char* in2, int k, bool verbo
   names.insert(names.end(), n2.begin(), n2.end());
   std::vector<const char*> ptrs;
   for (const auto& n : names) ptrs.push_back(n.c_str());
-  klsh_khtable_stats st;
+  klsh_khtable_stats st{};
+  st.struct_size = sizeof(st);
   check(klsh_build_khtable(ctx, ptrs.data(), (int)ptrs.size(), k, "", &st), "klsh_build_khtable");
   if (verbose)
     printf("k-mer table: %llu k-mers from %llu records of %zu databases (%.1f ms, %.1f ms reading)\n",
@@ -270,7 +272,8 @@ int run_extract(klsh_ctx* ctx, const std::vector<std::string>& s1,
       const std::string out = pre + "_" + base;
       if (verbose) printf("writing to %s\n", out.c_str());
       fflush(stdout);
-      klsh_extract_stats st;
+      klsh_extract_stats st{};
+      st.struct_size = sizeof(st);
       check(klsh_extract_fastq(ctx, g == 0 ? set1 : set2, path.c_str(), out.c_str(), k, vote, &st),
             "klsh_extract_fastq");
       if (verbose)

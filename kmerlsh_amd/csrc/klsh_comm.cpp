@@ -145,10 +145,6 @@ Comm* make_rccl_comm(int rank, int world, const void* unique_id, int device, std
   auto c = std::make_unique<RcclComm>();
   c->rank = rank;
   c->world = world;
-  if (const char* e = getenv("KLSH_COMM_TIMEOUT_S")) {
-    const double v = atof(e);
-    if (v > 0.0) c->timeout_s = v;
-  }
   const ncclResult_t r = ncclCommInitRank(&c->nc, world, id, rank);
   if (r != ncclSuccess) {
     if (err) *err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);

@@ -57,7 +57,7 @@ struct Comm {
     }
     return 0;
   }
-  double timeout_s = 600.0;  // KLSH_COMM_TIMEOUT_S
+  double timeout_s = 600.0;  // option "comm_timeout_s"
   bool aborted = false;
   std::string err;
 };

@@ -103,10 +103,7 @@ struct klsh_ctx {
   klsh::KStampBlock* kstamp = nullptr;
   uint64_t kt_iter = 0;
   klsh::LookBack lb{nullptr, 0};  // the one-launch compaction of small iterations
-  bool kernel_timing = [] {
-    const char* e = getenv("KLSH_KERNEL_TIMING");
-    return !(e && e[0] == '0');
-  }();
+  bool kernel_timing = true;  // option "kernel_timing"
 
   // sizes
   int d = 0, dp = 0;
@@ -180,29 +177,34 @@ struct klsh_ctx {
   bool spec_swap = false;  // the queued keys went to keys2 (this iteration's sorted keys were in keys)
   bool zero_copy = true;
   klsh::RunCounters* rc = nullptr;  // run-list counters (device, one 128-B line each)
-  // fp16 image of the rows for the projection's screen (Rows::xh; KLSH_SHADOW=0: off); every row
-  // store of the merge kernels writes it too (store_row4 / store_row1)
-  bool shadow_on = [] {
-    const char* e = getenv("KLSH_SHADOW");
-    return !(e && atoi(e) == 0);
-  }();
+  // fp16 image of the rows for the projection's screen (Rows::xh), kept at d = 16, 32, 64 unless
+  // option "projection" asks for the exact packed chains; every row store of the merge kernels
+  // writes it too (store_row4 / store_row1)
   uint16_t* xh_alloc = nullptr;
+  bool shadow_wanted(int d_) const {
+    return pw.variant != klsh::kProjPacked && klsh::shadow_width_ok(d_);
+  }
+  // Queued tail batches (run_batched; option "tail_batch", default on)
+  bool tail_batch = true;
+  // klsh_hash_keys diagnostics (klsh_get_option): the projection kernel of the last call and
+  // the (row, hyperplane) pairs its screen left to the exact chains
+  int last_hash_kernel = klsh::kPkNone;
+  uint64_t last_hash_close = 0;
 
   ~klsh_ctx() { release(); }
 
   // Per-phase HIP events (sort / merge / compaction) cost latency in every iteration — an event
   // record on the stream is tens of microseconds in the small late iterations — so they are on
   // only with KLSH_PHASE_TIMING=1.  The projection is always bracketed (bench.py's roofline).
-  bool phase_timing = [] {
-    const char* e = getenv("KLSH_PHASE_TIMING");
-    return e && e[0] == '1';
-  }();
+  bool phase_timing = false;  // option "phase_timing"
 
   // Sharded loop: below this many live rows the per-iteration exchanges cost more than they save
   // (the late iterations are latency-bound on one GPU already), so every rank takes the whole
   // canonical order and runs the remaining iterations on its replica — identically, with no
   // communication.  klsh_set_option(ctx, "shard_min_rows", n); 0 = always sharded.
   uint64_t shard_min_rows = 1u << 21;
+  // option "comm_timeout_s": a collective that has not completed after this long aborts the group
+  double comm_timeout_s = 600.0;
 
   // "stop_after" (klsh_set_option): run only the first k iterations of a call's threshold
   // schedule (0 = all).  Prefix parity tests of the long configs use it; results of the
@@ -269,7 +271,6 @@ struct klsh_ctx {
     pw.cap = 0;
     for (auto& c : mw.big) dfree(c);
     for (auto& c : mw.cls) dfree(c);
-    for (auto& c : mw.act) dfree(c);
     dfree(kstamp);
     dfree(lb.status);
     dfree(xh_alloc);
@@ -324,7 +325,7 @@ struct klsh_ctx {
       dp = dp_;
       rows.d = d;
       rows.dp = dp;
-      rows.xh = klsh::shadow_width_ok(d) ? xh_alloc : nullptr;
+      rows.xh = shadow_wanted(d) ? xh_alloc : nullptr;
       drop_snapshot();
       return 0;
     }
@@ -346,15 +347,14 @@ struct klsh_ctx {
       release_state();
       return e;
     }
-    if (shadow_on && klsh::shadow_width_ok(d_)) {  // (in the large-buffer group: see below)
+    if (shadow_wanted(d_)) {  // (in the large-buffer group: see below)
       if ((e = dalloc(&xh_alloc, s * dp_))) {
         release_state();
         return e;
       }
     }
     for (int c = 0; c < klsh::kGroupClasses; ++c) {
-      if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s))) ||
-          (e = dalloc(&mw.act[c], klsh::group_class_capacity(c, s)))) {
+      if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s)))) {
         release_state();
         return e;
       }
@@ -397,7 +397,23 @@ struct klsh_ctx {
     dp = dp_;
     rows.d = d;
     rows.dp = dp;
-    rows.xh = klsh::shadow_width_ok(d) ? xh_alloc : nullptr;
+    rows.xh = shadow_wanted(d) ? xh_alloc : nullptr;
+    return 0;
+  }
+  // Option "projection" changed: keep the fp16 image (allocated and rebuilt from x) or drop it.
+  int apply_projection_variant() {
+    if (!cap_slots) return 0;  // nothing reserved yet: reserve() decides
+    if (shadow_wanted(d)) {
+      if (!xh_alloc) {
+        if (int e = dalloc(&xh_alloc, cap_slots * (uint64_t)cap_dp)) return e;
+      }
+      rows.xh = xh_alloc;
+      klsh::launch_shadow_build(rows, slots, stream);  // merges did not keep it while it was off
+      KLSH_HIP(hipGetLastError());
+      KLSH_HIP(hipStreamSynchronize(stream));
+    } else {
+      rows.xh = nullptr;
+    }
     return 0;
   }
 
@@ -536,14 +552,8 @@ static void count_class_rows(klsh_stats* st, const Counters& c, uint64_t n, bool
     st->kern[KC_TAIL].runs += small_runs + big_runs;
     return;
   }
-  if (c.screened) {  // the screen saw every small run, the merge only the ones it passed
-    st->kern[KC_SCREEN].rows += c.n_small_rows;
-    st->kern[KC_SCREEN].runs += small_runs;
-    st->kern[KC_SMALL].rows += c.n_act_rows;
-  } else {
-    st->kern[KC_SMALL].rows += c.n_small_rows;
-    st->kern[KC_SMALL].runs += small_runs;
-  }
+  st->kern[KC_SMALL].rows += c.n_small_rows;
+  st->kern[KC_SMALL].runs += small_runs;
   for (int b = 0; b < kBigClasses; ++b) {
     st->kern[KC_BIG128 + b].rows += c.n_big_rows[b];
     st->kern[KC_BIG128 + b].runs += c.n_big[b];
@@ -579,7 +589,8 @@ int set_error(int code, const char* msg) { return fail(code, msg); }
 extern "C" {
 
 const char* klsh_last_error(void) { return g_err.c_str(); }
-const char* klsh_version(void) { return "klsh-mi355x 0.1 (gfx950)"; }
+const char* klsh_version(void) { return "klsh-mi355x 0.2 (gfx950)"; }
+int klsh_abi_version(void) { return KLSH_ABI_VERSION; }
 
 klsh_ctx* klsh_create(int device, int* err) {
   auto set = [&](int e) {
@@ -624,13 +635,9 @@ klsh_ctx* klsh_create(int device, int* err) {
   // its own system-scope release).  A default event ends with a system-scope release — an L2
   // writeback of everything the kernel before it wrote, 6-16 us of stream time per event on C2
   // (the projection -> sort and fork / join gaps of the round-3 trace) — so timing events skip
-  // the fence and the fork / join events release at device scope (KLSH_EVENT_FENCE=1: defaults).
-  static const bool fence = [] {
-    const char* e = getenv("KLSH_EVENT_FENCE");
-    return e && atoi(e) != 0;
-  }();
-  const unsigned tflags = fence ? hipEventDefault : hipEventDisableSystemFence;
-  const unsigned oflags = hipEventDisableTiming | (fence ? 0u : hipEventReleaseToDevice);
+  // the fence and the fork / join events release at device scope.
+  const unsigned tflags = hipEventDisableSystemFence;
+  const unsigned oflags = hipEventDisableTiming | hipEventReleaseToDevice;
   for (auto& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, tflags) == hipSuccess;
   for (auto& e : c->sev) ok = ok && hipEventCreateWithFlags(&e, tflags) == hipSuccess;
   for (int i = 0; i < klsh::kMergeStreams; ++i) {
@@ -898,7 +905,7 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
     KLSH_HIP(hipEventSynchronize(ctx->sev[1]));
     st->small_ms += elapsed(ctx->sev[0], ctx->sev[1]);
     st->small_launches += 1;
-    st->small_rows += ctx->h_ctr->screened ? ctx->h_ctr->n_act_rows : ctx->h_ctr->n_small_rows;
+    st->small_rows += ctx->h_ctr->n_small_rows;
     st->small_iter_merges += n - ctx->h_ctr->total;
   }
   if (timed && zc) KLSH_HIP(hipEventSynchronize(ctx->ev[4]));
@@ -999,15 +1006,13 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
 // ring slot and the host reads a chunk's slots when its last sequence number is in — the trace,
 // the RNG counter and the statistics come out exactly as the per-iteration loop's.
 static bool batch_eligible(const klsh_ctx* ctx, uint64_t n, int bucket_thr, int iters_left) {
-  static const bool on = [] {
-    const char* e = getenv("KLSH_TAIL_BATCH");
-    return !(e && atoi(e) == 0);
-  }();
-  if (!on || n < 2 || n >= (1u << 20) || iters_left < 2) return false;
+  if (!ctx->tail_batch || n < 2 || n >= (1u << 20) || iters_left < 2) return false;
   if (bucket_thr >= 0 && n > (uint64_t)bucket_thr) return false;
   if (!ctx->zero_copy || !ctx->ring_dev || !ctx->lb.status || ctx->phase_timing) return false;
   if (!klsh::project_device_n_ok(ctx->d) || ctx->mw.dlist) return false;
+#ifdef KLSH_DIAG
   if (getenv("KLSH_BUCKET_STATS") || getenv("KLSH_ITER_LOG")) return false;
+#endif
   // every queued iteration's hyperplanes resident at once
   return (uint64_t)iters_left * (uint64_t)floor_log2(n) * (uint64_t)ctx->dp <= (64ull << 20);
 }
@@ -1094,6 +1099,7 @@ static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, 
       const int h = floor_log2(n_in);
       if (nt_trace) nt_trace[ch.it0 + c] = n_in;
       st->iterations += 1;
+      st->project_launches += 1;  // (no HIP events around queued launches: not in project_ms)
       *rng_counter += (uint64_t)h;
       st->hyperplanes += (uint64_t)h;
       st->sum_rows += n_in;
@@ -1117,10 +1123,14 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
                       int bucket_size_threshold, uint32_t seed_base, uint64_t* rng_counter,
                       uint64_t* nt_trace, klsh_stats* st) {
   hipStream_t s = ctx->stream;
-  static FILE* iter_log = [] {  // diagnostics: per-iteration wall time (it, n, h, ms)
+#ifdef KLSH_DIAG  // diagnostics build: per-iteration wall time (it, n, h, ms)
+  static FILE* iter_log = [] {
     const char* e = getenv("KLSH_ITER_LOG");
     return e ? fopen(e, "a") : nullptr;
   }();
+#else
+  FILE* const iter_log = nullptr;
+#endif
   // per-class timing: iteration `it` uses set it & 1 (its queued projection included); the
   // previous iteration's set is read once this one's work is queued
   // per-class stamps: the call's iterations stamp sets 0, 1, 0, ... in turn (ctx->kt_iter); a
@@ -1177,6 +1187,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
                      &fk, &fv, s, ktime(j));
     KLSH_HIP(hipGetLastError());
     if (ctx->phase_timing) KLSH_HIP(hipEventRecord(ctx->ev[5], s));
+#ifdef KLSH_DIAG
     if (const char* path = getenv("KLSH_BUCKET_STATS")) {  // diagnostics: run-length histogram
       std::vector<uint32_t> hk(n);
       KLSH_HIP(hipMemcpyAsync(hk.data(), fk, 4 * n, hipMemcpyDeviceToHost, s));
@@ -1204,13 +1215,19 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
         fclose(f);
       }
     }
+#endif
     // Queue the next iteration's projection behind this compaction.  If this iteration turns out
     // to have oversize buckets (nestedCluster changes rows and draws hyperplanes first), the
     // queued keys are simply recomputed; they go to the key buffer the nested work is not reading
     // (this iteration's sorted keys fk stay intact), keys2 when fk is keys — the next iteration
     // then swaps the two pointers.
+#ifdef KLSH_DIAG
+    const bool diag_stats = getenv("KLSH_BUCKET_STATS") != nullptr;
+#else
+    const bool diag_stats = false;
+#endif
     const bool ahead = ctx->zero_copy && it + 1 < it_end &&
-                       klsh::project_device_n_ok(ctx->d) && !getenv("KLSH_BUCKET_STATS");
+                       klsh::project_device_n_ok(ctx->d) && !diag_stats;
     uint32_t* const spec_out = fk == ctx->keys ? ctx->keys2 : ctx->keys;
     const std::function<int(uint32_t*)> queue_next = [&](uint32_t* next_order) -> int {
       const uint64_t k_next = k + (uint64_t)h;  // h_next <= h: inside the drawn window
@@ -1235,15 +1252,27 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     if (ctx->spec_pending && *rng_counter != ctx->spec_k) {  // nested ran: recomputed next time
       ctx->spec_pending = false;
       ctx->spec_swap = false;
+      // the discarded launch stamped the next iteration's projection lines: clear them, or the
+      // recomputed projection's span would start at the discarded one (across the nested work)
+      if (ctx->kernel_timing && ctx->kstamp) {
+        klsh::KStampSet* set = &ctx->kstamp->set[ctx->kt_iter & 1u];
+        KLSH_HIP(hipMemsetAsync(&set->t0[klsh::KC_PROJECT][0], 0xFF,
+                                sizeof(set->t0[klsh::KC_PROJECT]), s));
+        KLSH_HIP(hipMemsetAsync(&set->t1[klsh::KC_PROJECT][0], 0,
+                                sizeof(set->t1[klsh::KC_PROJECT]), s));
+      }
     }
-    if (rec) st->project_ms += elapsed(ctx->ev[e0], ctx->ev[e0 + 1]);
+    if (rec) {
+      st->project_ms += elapsed(ctx->ev[e0], ctx->ev[e0 + 1]);
+      st->project_timed_launches += 1;
+    }
     if (rec && ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[1], ctx->ev[5]);
     st->project_launches += 1;
     st->sum_rows += n;
     st->sum_proj_bits += n * (uint64_t)h;
     st->sum_merges += n - ctx->n_live;
     threshold -= sim_step;
-    if (iter_log)
+    if (iter_log)  // (diagnostics build)
       fprintf(iter_log, "%d %llu %d %.4f %.4f %u %u %u %u\n", it, (unsigned long long)n, h,
               now_ms() - t_it, ctx->t_enqueued - t_it, ctx->h_ctr->n_big[0], ctx->h_ctr->n_big[1],
               ctx->h_ctr->n_big[2] + ctx->h_ctr->n_big[3], ctx->h_ctr->n_huge);
@@ -1480,6 +1509,7 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
     st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
     if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[6], ctx->ev[5]);
     st->project_launches += 1;
+    st->project_timed_launches += 1;
     st->sum_rows += N;
     st->sum_proj_bits += N * (uint64_t)h;
     st->sum_merges += N - N_next;
@@ -1537,9 +1567,13 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
     return fail(KLSH_E_STATE, "klsh_cluster before a load");
   }
   KLSH_HIP(hipSetDevice(ctx->device));
+  if (stats && stats->struct_size != sizeof(klsh_stats))
+    return fail(KLSH_E_ARG, "klsh_stats.struct_size != sizeof(klsh_stats): built against another "
+                            "klsh.h (KLSH_ABI_VERSION " + std::to_string(KLSH_ABI_VERSION) + ")");
   klsh_stats local{};
   klsh_stats* st = stats ? stats : &local;
   memset(st, 0, sizeof(*st));
+  st->struct_size = sizeof(*st);
   st->world = (uint64_t)ctx->world();
   ctx->mw.huge_cap = 0;  // (set per iteration from the run counts by the single-device loop)
   ctx->mw.dlist = nullptr;
@@ -1592,7 +1626,9 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   }
   st->n_final = ctx->n_live;
   st->wall_ms = now_ms() - t_start;
+#ifdef KLSH_MERGE_PROF
   if (getenv("KLSH_MERGE_PROF")) klsh::merge_prof_dump(stderr);
+#endif
   return 0;
 }
 
@@ -1610,6 +1646,7 @@ int klsh_comm_init(klsh_ctx* ctx, int rank, int world, const uint8_t* id) {
   std::string err;
   klsh::Comm* c = klsh::make_rccl_comm(rank, world, id, ctx->device, &err);
   if (!c) return fail(KLSH_E_HIP, err);
+  c->timeout_s = ctx->comm_timeout_s;
   ctx->release_shard();
   delete ctx->comm;
   ctx->comm = c;
@@ -1630,22 +1667,28 @@ int klsh_comm_init_local(klsh_ctx** ctxs, int world) {
   return 0;
 }
 
+// Options (include/klsh.h).  Results never depend on them, except that "stop_after" stops early.
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   if (!ctx || !name) return fail(KLSH_E_ARG, "null argument");
   const std::string n(name);
+  auto flag = [&](bool* f) {
+    *f = value != 0;
+    return 0;
+  };
+  // launch sizes (0 = the default): unsigned 32-bit, bounded so no grid overflows
+  auto grid = [&](uint32_t* g) {
+    if (value < 0 || value > (1 << 20)) return fail(KLSH_E_ARG, n + " must be in [0, 2^20]");
+    *g = (uint32_t)value;
+    return 0;
+  };
   if (n == "shard_min_rows") {
     if (value < 0) return fail(KLSH_E_ARG, "shard_min_rows must be >= 0");
     ctx->shard_min_rows = (uint64_t)value;
     return 0;
   }
-  if (n == "phase_timing") {
-    ctx->phase_timing = value != 0;
-    return 0;
-  }
-  if (n == "kernel_timing") {
-    ctx->kernel_timing = value != 0;
-    return 0;
-  }
+  if (n == "phase_timing") return flag(&ctx->phase_timing);
+  if (n == "kernel_timing") return flag(&ctx->kernel_timing);
+  if (n == "tail_batch") return flag(&ctx->tail_batch);
   if (n == "hyperplane_window") {
     if (value < 0) return fail(KLSH_E_ARG, "hyperplane_window must be >= 0");
     ctx->hyperplane_window = (uint64_t)value;
@@ -1656,7 +1699,54 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->stop_after = (int)value;
     return 0;
   }
+  if (n == "projection") {
+    if (value != klsh::kProjAuto && value != klsh::kProjPacked)
+      return fail(KLSH_E_ARG, "projection must be 0 (default) or 1 (exact packed chains)");
+    KLSH_HIP(hipSetDevice(ctx->device));
+    ctx->pw.variant = (uint32_t)value;
+    return ctx->apply_projection_variant();
+  }
+  if (n == "comm_timeout_s") {
+    if (value <= 0) return fail(KLSH_E_ARG, "comm_timeout_s must be > 0");
+    ctx->comm_timeout_s = (double)value;
+    if (ctx->comm) ctx->comm->timeout_s = (double)value;
+    return 0;
+  }
+  if (n == "h16_grid") return grid(&ctx->pw.h16_grid);
+  if (n == "h16_segcap") return grid(&ctx->pw.segcap);
+  if (n == "wide_grid") return grid(&ctx->pw.wide_grid);
+  if (n == "fix_grid") return grid(&ctx->pw.fix_grid);
+  if (n == "small_grid") return grid(&ctx->mw.small_grid);
+  if (n == "tail_big_groups") return grid(&ctx->mw.tail_nbig);
+  if (n == "tail_small_groups") return grid(&ctx->mw.tail_nsmall);
+  if (n == "wide_group_grid") return grid(&ctx->mw.wide_group_grid);
   return fail(KLSH_E_ARG, "unknown option " + n);
+}
+
+int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
+  if (!ctx || !name || !value) return fail(KLSH_E_ARG, "null argument");
+  const std::string n(name);
+  if (n == "shard_min_rows") *value = (int64_t)ctx->shard_min_rows;
+  else if (n == "phase_timing") *value = ctx->phase_timing;
+  else if (n == "kernel_timing") *value = ctx->kernel_timing;
+  else if (n == "tail_batch") *value = ctx->tail_batch;
+  else if (n == "hyperplane_window") *value = (int64_t)ctx->hyperplane_window;
+  else if (n == "stop_after") *value = ctx->stop_after;
+  else if (n == "projection") *value = ctx->pw.variant;
+  else if (n == "comm_timeout_s") *value = (int64_t)ctx->comm_timeout_s;
+  else if (n == "h16_grid") *value = ctx->pw.h16_grid;
+  else if (n == "h16_segcap") *value = ctx->pw.segcap;
+  else if (n == "wide_grid") *value = ctx->pw.wide_grid;
+  else if (n == "fix_grid") *value = ctx->pw.fix_grid;
+  else if (n == "small_grid") *value = ctx->mw.small_grid;
+  else if (n == "tail_big_groups") *value = ctx->mw.tail_nbig;
+  else if (n == "tail_small_groups") *value = ctx->mw.tail_nsmall;
+  else if (n == "wide_group_grid") *value = ctx->mw.wide_group_grid;
+  else if (n == "fp16_image") *value = ctx->rows.xh != nullptr;
+  else if (n == "last_hash_kernel") *value = ctx->last_hash_kernel;
+  else if (n == "last_hash_close_pairs") *value = (int64_t)ctx->last_hash_close;
+  else return fail(KLSH_E_ARG, "unknown option " + n);
+  return 0;
 }
 
 int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world) {
@@ -1724,11 +1814,17 @@ int klsh_result(klsh_ctx* ctx, float* rows, uint64_t* member_offsets, uint64_t* 
   return 0;
 }
 
+// The projection kernels the loop uses, on caller rows: the same dispatch (launch_project) with
+// the context's projection options, the fp16 row image built from the rows where the loop keeps
+// one (d = 16, 32, 64), so the certified screens and their exact fix-up paths are what a test of
+// this entry point exercises.
 int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const float* table, int h,
                    uint32_t* keys) {
   if (!ctx || (!rows && n) || (!keys && n) || (!table && h > 0)) return fail(KLSH_E_ARG, "null argument");
   if (d <= 0 || d > 4096 || h < 0 || h > 31) return fail(KLSH_E_RANGE, "d or h out of range");
   if (n >= 0xFFFFFFF0ull) return fail(KLSH_E_RANGE, "rows >= 2^32");
+  ctx->last_hash_kernel = klsh::kPkNone;
+  ctx->last_hash_close = 0;
   if (n == 0) return 0;
   KLSH_HIP(hipSetDevice(ctx->device));
   const int dp = (d + 3) & ~3;
@@ -1737,15 +1833,23 @@ int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const fl
   r.dp = dp;
   uint32_t *slots = nullptr, *dkeys = nullptr;
   float* W = nullptr;
-  klsh::ProjectWork pw{};
+  uint16_t* xh = nullptr;
+  klsh::ProjectWork pw = ctx->pw;  // the context's launch options, fresh workspaces
+  pw.fix = nullptr;
+  pw.ws = nullptr;
+  auto release = [&] {
+    dfree(r.x); dfree(slots); dfree(dkeys); dfree(W); dfree(pw.fix); dfree(pw.ws); dfree(xh);
+  };
   int e = 0;
+  const bool image = ctx->shadow_wanted(d);
   if ((e = dalloc(&r.x, n * dp)) || (e = dalloc(&slots, n)) || (e = dalloc(&dkeys, n)) ||
       (e = dalloc(&W, (uint64_t)std::max(h, 1) * dp)) || (e = dalloc(&pw.fix, n)) ||
-      (e = dalloc(&pw.ws, 64))) {
-    dfree(r.x); dfree(slots); dfree(dkeys); dfree(W); dfree(pw.fix); dfree(pw.ws);
+      (e = dalloc(&pw.ws, 64)) || (image && (e = dalloc(&xh, n * dp)))) {
+    release();
     return e;
   }
   pw.cap = (uint32_t)n;
+  r.xh = xh;
   hipStream_t s = ctx->stream;
   std::vector<uint32_t> iota(n);
   for (uint64_t i = 0; i < n; ++i) iota[i] = (uint32_t)i;
@@ -1759,14 +1863,27 @@ int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const fl
       hipMemcpyAsync(slots, iota.data(), 4 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
     rc = fail(KLSH_E_HIP, "upload");
   } else {
-    klsh::launch_project(r, slots, dkeys, (uint32_t)n, W, h, 0u, s, &pw);
+    if (image) klsh::launch_shadow_build(r, n, s);
+    const int kern = klsh::launch_project(r, slots, dkeys, (uint32_t)n, W, h, 0u, s, &pw);
+    uint32_t w[64];
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(keys, dkeys, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+        hipMemcpyAsync(w, pw.ws, sizeof(w), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
       rc = fail(KLSH_E_HIP, "projection");
+    } else {
+      // close calls: ws[4..6) the wide-row fix-up total, ws[32..64) the fp16 screen's counters
+      unsigned long long fixed = 0, part = 0;
+      for (int i : {4, 32, 34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62}) {
+        memcpy(&part, w + i, sizeof(part));
+        fixed += part;
+      }
+      ctx->last_hash_kernel = kern;
+      ctx->last_hash_close = fixed;
+    }
   }
   (void)hipStreamSynchronize(s);
-  dfree(r.x); dfree(slots); dfree(dkeys); dfree(W); dfree(pw.fix); dfree(pw.ws);
+  release();
   return rc;
 }
 

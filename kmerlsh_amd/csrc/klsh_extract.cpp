@@ -683,7 +683,10 @@ int klsh_extract_fastq(klsh_ctx* ctx, const klsh_kset* ks, const char* in_path,
     return set_error(KLSH_E_ARG, "bad argument");
   if (k < 1 || k > 32) return set_error(KLSH_E_RANGE, "k must be in [1, 32] (Kmer::MAX_K)");
   const double t_start = now_ms();
+  if (st && st->struct_size != sizeof(klsh_extract_stats))
+    return set_error(KLSH_E_ARG, "klsh_extract_stats.struct_size != sizeof: built against another klsh.h");
   klsh_extract_stats local{};
+  local.struct_size = sizeof(local);
   KLSH_XHIP(hipSetDevice(klsh::ctx_device(ctx)));
   const hipStream_t s = klsh::ctx_stream(ctx);
   FastqReader rdr;

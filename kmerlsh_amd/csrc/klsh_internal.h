@@ -51,9 +51,6 @@ struct alignas(128) CountLine {
 struct RunCounters {
   CountLine n_seg, n_cls[kGroupClasses], n_big[kBigClasses], n_huge, n_over, n_small_rows;
   CountLine n_big_rows[kBigClasses], n_huge_rows;  // rows in the big / huge runs (kernel rooflines)
-  // the small-run screen (k_small_screen): runs of each class it could not rule out, their rows,
-  // and a flag that it ran this iteration
-  CountLine n_act[kGroupClasses], n_act_rows, screened;
 };
 
 // Run-finding workspace (u32 words) for `slots` positions: 19 counts + a tail end + a 4096-bit
@@ -73,8 +70,6 @@ struct Counters {
   uint32_t n_small_rows;           // rows in the runs of 2..64 rows (the small-run merge's rows)
   uint32_t n_big_rows[kBigClasses];  // rows in the runs of each big class
   uint32_t n_huge_rows;            // rows in the runs of k_merge_huge
-  uint32_t n_act_rows;             // rows in the small runs the screen passed to k_merge_small
-  uint32_t screened;               // 1: the small-run screen ran this iteration
 };
 
 // Per-kernel-class timing (bench.py's roofline) from in-kernel stamps: every workgroup of a timed
@@ -89,7 +84,7 @@ struct Counters {
 // order) and clears it; the engine folds the last set at the end of a call.
 enum KClass : int {
   KC_PROJECT = 0, KC_SORT, KC_RUNS, KC_SMALL, KC_BIG128, KC_BIG192, KC_BIG384, KC_BIG896, KC_HUGE,
-  KC_TAIL, KC_COMPACT, KC_PAIRS, KC_SCREEN, KC_COUNT
+  KC_TAIL, KC_COMPACT, KC_COUNT
 };
 constexpr int kStampSlots = 16;
 struct alignas(128) StampLine {
@@ -118,10 +113,6 @@ constexpr KTime kNoTime{nullptr, 0, -1};
 // Merge workspace (device), sized for `cap` positions.
 struct MergeWork {
   uint2* cls[kGroupClasses];       // (start, length) of runs per size class
-  // the runs of each class the fp16 screen could not rule out (k_small_screen), and whether the
-  // small-run merge reads these instead of cls (set per launch)
-  uint2* act[kGroupClasses];
-  uint32_t screened;
   uint2* big[kBigClasses];         // (start, length) of runs for k_merge_big, per class
   uint2* huge;                     // (start, length) of runs for k_merge_huge
   uint2* over;                     // (start, length) of oversize runs
@@ -144,6 +135,11 @@ struct MergeWork {
   // engine sets a cap of 64 after an iteration without such runs: an empty launch of hundreds of
   // 512-lane workgroups waits for CUs behind the other classes (C2: 25 ms per step of span)
   uint32_t huge_cap;
+  // launch sizes (klsh_set_option; 0 = the measured default, see the launch code)
+  uint32_t small_grid;       // "small_grid": the small-run merge's persistent launch
+  uint32_t tail_nbig;        // "tail_big_groups": k_merge_tail's big-run workgroups
+  uint32_t tail_nsmall;      // "tail_small_groups": k_merge_tail's small-run workgroups
+  uint32_t wide_group_grid;  // "wide_group_grid": the wide-row group merges, per class
   hipStream_t aux[3];
   KTime kt;                // per-class stamps of this iteration's merge launches
   hipEvent_t small_ev[2];  // HIP events around the small-run launch (nullptr: not recorded)
@@ -200,7 +196,19 @@ struct ProjectWork {
   uint2* fix;
   uint32_t* ws;
   uint32_t cap;
+  // launch sizes and test hooks (klsh_set_option; 0 = default)
+  uint32_t h16_grid;   // "h16_grid": fp16-image projection workgroups, at most
+  uint32_t wide_grid;  // "wide_grid": wide-row screen workgroups, at most
+  uint32_t fix_grid;   // "fix_grid": wide-row fix-up workgroups
+  uint32_t segcap;     // "h16_segcap" (tests): fix-up entries per fp16-projection workgroup
+  uint32_t variant;    // "projection": kProjAuto / kProjPacked / kProjScreen (set per launch)
 };
+// Projection variants (klsh_set_option "projection"): the default picks the certified
+// matrix-core screen where it exists (the fp16 row image at d = 16 / 32 / 64, bf16x3 above 64)
+// and the packed exact VALU chains elsewhere; kProjPacked forces the exact chains (no fp16 image
+// is kept then); kProjScreen asks for the screen (an error where none exists).  Keys are the
+// same bits either way.
+constexpr uint32_t kProjAuto = 0, kProjPacked = 1, kProjScreen = 2;
 // workgroups of the fp16-image projection, at most (C2 per step: 2048 -> 46.1, 4096 -> 46.5,
 // 8192 -> 48.5, 16384 -> 52.9, 32768 -> 55.5 ms, interleaved on one box)
 constexpr uint32_t kH16Grid = 2048;
@@ -218,10 +226,12 @@ void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* key
                              KTime kt = kNoTime, const uint32_t* woff_dev = nullptr,
                              const ProjectWork* pw = nullptr);
 
-// pw (may be null): the workspace that enables the matrix-core kernel for wide rows (d > 64).
-void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
-                    const float* W, int h, uint32_t key_or, hipStream_t s,
-                    const ProjectWork* pw = nullptr, KTime kt = kNoTime);
+// pw (may be null): the workspace that enables the matrix-core screens (the fp16 row image where
+// r.xh is set, bf16x3 for d > 64).  Returns the kernel it launched (ProjKernel).
+enum ProjKernel : int { kPkNone = -1, kPkPacked = 0, kPkH16 = 1, kPkWide = 2 };
+int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
+                   const float* W, int h, uint32_t key_or, hipStream_t s,
+                   const ProjectWork* pw = nullptr, KTime kt = kNoTime);
 
 // Stable LSD radix sort of (keys, vals)[0..n) on the low `bits` bits (klsh_sort.hip); ping-pong
 // buffers, *out_k/*out_v = the pair holding the result.  ws: sort_ws_words(n) words.

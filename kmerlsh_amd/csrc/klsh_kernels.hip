@@ -294,13 +294,11 @@ __global__ __launch_bounds__(256) void k_project_generic(const float* __restrict
   kt_end(kt, KC_PROJECT);
 }
 
-// Matrix-core projection, certified.  S = X W^T for 32 rows x 32 hyperplanes per wave with the
-// bf16x3 split (x = hi + lo; hi.hi + hi.lo + lo.hi, f32 accumulation) on v_mfma_f32_32x32x16_bf16.
-// |S - s| <= eps * |w| |x| against the reference's sequential f32 sum s (eps from
-// project_eps(d)), so every sign with |S| > eps |w| |x| is the reference's bit; the rest (about
-// 1e-3 of the row-hyperplane pairs, and any NaN or tiny row) take the exact sequential chain.
-// The row norms come from the loaded row itself (approximate, only a bound).  The sign bits of a
-// row across its hyperplanes come out of one wave ballot per accumulator register.
+// Matrix-core projection of f32 rows (wide rows, k_project_mfma_wide below), certified: S = X W^T
+// with the bf16x3 split (x = hi + lo; hi.hi + hi.lo + lo.hi, f32 accumulation) on
+// v_mfma_f32_32x32x16_bf16.  |S - s| <= eps * |w| |x| against the reference's sequential f32 sum
+// s (eps from project_eps(d)), so every sign with |S| > eps |w| |x| is the reference's bit; the
+// rest (and any NaN, tiny or huge row) take the exact sequential chain.
 typedef __bf16 pbf16x8 __attribute__((ext_vector_type(8)));
 typedef float pf32x16 __attribute__((ext_vector_type(16)));
 
@@ -324,117 +322,6 @@ float project_eps(int d) {
   return 1.5f * (3.03f * 0x1p-16f + (17.0f + 3.0f * ks) * 0x1p-23f + (float)(d + 1) * 0x1p-24f);
 }
 
-template <int D>
-__global__ __launch_bounds__(256) void k_project_mfma(const float* __restrict__ X, int dp,
-                                                      const uint32_t* __restrict__ slots,
-                                                      uint32_t* __restrict__ keys, uint32_t n,
-                                                      const float* __restrict__ W, int h,
-                                                      uint32_t key_or, float eps) {
-  constexpr int ST = D + 4;
-  constexpr int KS = D / 16;  // k-steps of 16
-  __shared__ __attribute__((aligned(16))) float sw[32 * ST];  // hyperplane j at row j (0 if j >= h)
-  __shared__ float swn[32];                                    // |w_j| (a bound)
-  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, r = lane & 31u, hh = lane >> 5;
-  for (int i = (int)t; i < 32 * D; i += 256) {
-    const int j = i / D, k = i % D;
-    sw[j * ST + k] = j < h ? W[(size_t)j * dp + k] : 0.0f;
-  }
-  __syncthreads();
-  if (t < 32) {
-    float a = 0.0f;
-    for (int k = 0; k < D; ++k) a += sw[t * ST + k] * sw[t * ST + k];
-    swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;  // a bound: the hardware sqrt (1 ulp) suffices
-  }
-  __syncthreads();
-  // this lane's B fragments: hyperplane r, k = 16s + 8hh + e
-  pbf16x8 bh[KS], bl[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const float* wp = sw + r * ST + 16 * s + 8 * hh;
-    psplit8(*reinterpret_cast<const float4*>(wp), *reinterpret_cast<const float4*>(wp + 4), bh[s], bl[s]);
-  }
-  const float wn = swn[r];
-  const bool col_ok = (int)r < h;
-  // rows of the wave's next group are loaded while the current group is computed
-  const uint32_t step = gridDim.x * 128u;
-  uint32_t g0 = (blockIdx.x * 4u + wv) * 32u;
-  float4 xa[KS][2];
-  auto load_group = [&](uint32_t g) {
-    if (g >= n) return;
-    const uint32_t rw = g + r;
-    const float* xr = X + (size_t)slots[rw < n ? rw : g] * dp + 8 * hh;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      xa[s][0] = *reinterpret_cast<const float4*>(xr + 16 * s);
-      xa[s][1] = *reinterpret_cast<const float4*>(xr + 16 * s + 4);
-    }
-  };
-  load_group(g0);
-  for (; g0 < n; g0 += step) {
-    const uint32_t row = g0 + r;
-    const bool valid = row < n;
-    pbf16x8 ah[KS], al[KS];
-    float ss = 0.0f;  // this lane's half of |x|^2 (a bound only)
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      psplit8(xa[s][0], xa[s][1], ah[s], al[s]);
-      ss += xa[s][0].x * xa[s][0].x + xa[s][0].y * xa[s][0].y + xa[s][0].z * xa[s][0].z +
-            xa[s][0].w * xa[s][0].w + xa[s][1].x * xa[s][1].x + xa[s][1].y * xa[s][1].y +
-            xa[s][1].z * xa[s][1].z + xa[s][1].w * xa[s][1].w;
-    }
-    load_group(g0 + step);
-    pf32x16 acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bh[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], bl[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], bh[s], acc, 0, 0, 0);
-    }
-    ss += __shfl_xor(ss, 32, 64);
-    const float xn = __builtin_amdgcn_sqrtf(ss) * 1.001f;  // >= |x| of row g0 + r
-    // acc[i] = S[row (i&3) + 8(i>>2) + 4hh][hyperplane r]; lane L < 32 collects row g0 + L
-    uint32_t bits = 0u, amb = 0u;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const uint32_t ri = (i & 3) + 8u * (i >> 2) + 4u * hh;
-      const float xni = __shfl(xn, (int)ri, 64);
-      const float sv = acc[i];
-      const float bound = eps * wn * xni;
-      const bool pos = col_ok && sv >= 0.0f;
-      // NaN, a tiny or huge row, or |S| within the bound: the exact chain decides
-      const bool am = col_ok && (!(__builtin_fabsf(sv) > bound) || !(xni >= 0x1p-60f) ||
-                                 !(xni <= 0x1p60f));
-      const uint64_t bp = __ballot(pos), ba = __ballot(am);
-      const uint32_t r0 = (i & 3) + 8u * (i >> 2);
-      if (lane == r0) {
-        bits = (uint32_t)bp;
-        amb = (uint32_t)ba;
-      }
-      if (lane == r0 + 4u) {
-        bits = (uint32_t)(bp >> 32);
-        amb = (uint32_t)(ba >> 32);
-      }
-    }
-    if (lane < 32 && valid) {
-      if (amb) {  // rare: the reference's sequential chains (hash/lshash.cc:44-51)
-        const float* x = X + (size_t)slots[row] * dp;
-        while (amb) {
-          const int j = __builtin_ctz(amb);
-          amb &= amb - 1u;
-          const float* w = sw + j * ST;
-          float sd = 0.0f;
-          for (int k = 0; k < D; ++k) sd = sd + w[k] * x[k];
-          bits = sd >= 0.0f ? (bits | (1u << j)) : (bits & ~(1u << j));
-        }
-      }
-      // hyperplane 0 is the key's most significant bit
-      keys[row] = (h > 0 ? (__builtin_bitreverse32(bits) >> (32 - h)) : 0u) | key_or;
-    }
-  }
-}
-
 // The projection from the fp16 row image (Rows::xh), certified.  x~ = fp16(x) is read (2d bytes a
 // row, half the f32 row gather) and S = x~ . w is taken on v_mfma_f32_32x32x16_f16 with w split
 // into fp16 hi + lo (two MFMAs per 16 columns; x~ needs no split).  Against the reference's
@@ -447,8 +334,8 @@ __global__ __launch_bounds__(256) void k_project_mfma(const float* __restrict__ 
 // 1.5x headroom; |x| <= 1.001 |x~| covers the 2^-11).  Signs with |S| above the bound are the
 // reference's bits; the rest (fp16 overflow, NaN, |S| within the bound: ~0.5 % of the
 // row-hyperplane pairs at d = 64) go to the fix-up list (k_project_fix: the exact chains on the
-// f32 row).  Layout as k_project_mfma: 32 rows x 32 hyperplanes per wave, one ballot per
-// accumulator register; the next group's rows are loaded during the current group.
+// f32 row).  32 rows x 32 hyperplanes per MFMA tile; the next group's rows are loaded during the
+// current group.
 typedef _Float16 ph16x8 __attribute__((ext_vector_type(8)));
 
 float h16_eps(int d) {
@@ -845,12 +732,10 @@ static void launch_h16(const Rows& r, const uint32_t* slots, uint32_t* keys, uin
                        const float* W, int h, uint32_t key_or, hipStream_t s,
                        const ProjectWork& pw, KTime kt, const uint32_t* n_dev,
                        const uint32_t* woff_dev) {
-  static const uint32_t gmax = [] {  // (KLSH_H16_GRID: A/B of the launch size)
-    const char* e = getenv("KLSH_H16_GRID");
-    return e ? (uint32_t)std::max(256, atoi(e)) : kH16Grid;
-  }();
+  const uint32_t gmax = pw.h16_grid ? std::max(256u, pw.h16_grid) : kH16Grid;  // "h16_grid"
   const uint32_t grid = std::min<uint32_t>((n + 255) / 256, gmax);
-  const uint32_t segcap = (pw.cap / 2) / grid;  // 16-B fix-up entries per workgroup
+  uint32_t segcap = (pw.cap / 2) / grid;  // 16-B fix-up entries per workgroup
+  if (pw.segcap) segcap = std::min(segcap, pw.segcap);  // "h16_segcap" (tests: the in-place path)
   const float eps = h16_eps(r.d), abs_c = h16_abs(r.d);
   auto go = [&](auto screen) {
     screen<<<grid, 256, 0, s>>>(r.xh, r.x, r.dp, slots, keys, n, W, h, key_or, eps, abs_c, pw,
@@ -862,7 +747,7 @@ static void launch_h16(const Rows& r, const uint32_t* slots, uint32_t* keys, uin
 }
 
 static bool h16_ok(const Rows& r, const ProjectWork* pw) {
-  return pw && r.xh && shadow_width_ok(r.d);
+  return pw && pw->variant != kProjPacked && r.xh && shadow_width_ok(r.d);
 }
 
 bool project_device_n_ok(int d) {
@@ -890,25 +775,16 @@ void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* key
   }
 }
 
-// The projection of a call: d in {8, 16, 32, 64} the packed VALU kernel (or, with
-// KLSH_PROJECT=mfma, the certified matrix-core kernel, bit-exact but measured slower at d <= 64:
-// 161-167 vs 140-145 us per C2 launch — its per-pair bound test and ballots cost what the packed
-// chains cost); wider rows the certified matrix-core screen + exact fix-up pass (pw given), else
-// the packed wide-row kernel (hyperplanes in LDS), else the generic kernel.
-static bool project_mfma_requested() {
-  static const bool v = [] {
-    const char* e = getenv("KLSH_PROJECT");
-    return e && std::string(e) == "mfma";
-  }();
-  return v;
-}
-
-void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
+// The projection of a call: the certified matrix-core screens where they exist (the fp16 row
+// image at d = 16, 32, 64; the bf16x3 screen + exact fix-up pass above 64), else the packed exact
+// VALU chains (d = 8 and any d without a screen, or option "projection" = kProjPacked): the
+// wide-row packed kernel with the hyperplanes in LDS, else the generic kernel.
+int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
                     const float* W, int h, uint32_t key_or, hipStream_t s, const ProjectWork* pw,
                     KTime kt) {
-  if (n == 0) return;
+  if (n == 0) return kPkNone;
   const dim3 grid((n + 255) / 256), block(256);
-  if (pw && r.d > 64 && h > 0) {
+  if (pw && pw->variant != kProjPacked && r.d > 64 && h > 0) {
     const size_t lds = (size_t)((r.d + 15) / 16) * 64 * 2 * 16 + 32 * sizeof(float);
     const size_t flds = sizeof(float) * (size_t)h * r.dp;  // the fix-up kernel's hyperplanes
     if (lds <= 96 * 1024 && flds <= 128 * 1024) {
@@ -919,42 +795,24 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
                               hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) == hipSuccess;
       (void)lds_ok;
       const uint32_t groups = (n + kWideNT / 2 - 1) / (kWideNT / 2);  // 32 rows per wave
-      static const uint32_t wcap = [] {  // (KLSH_WIDE_GRID: A/B of the launch size)
-        const char* e = getenv("KLSH_WIDE_GRID");
-        // one resident round (2 workgroups of 6 waves per CU): C5 projection 1203 -> 1076 ms per
-        // step (256..8192 swept on one box: 256 -> 1073, 512 -> 1076, 1024 -> 1112, 2048 -> 1203,
-        // 4096 -> 1318, 8192 -> 1533)
-        return e ? (uint32_t)std::max(64, atoi(e)) : 512u;
-      }();
+      // option "wide_grid": one resident round (2 workgroups of 6 waves per CU): C5 projection
+      // 1203 -> 1076 ms per step (256..8192 swept on one box: 256 -> 1073, 512 -> 1076, 1024 ->
+      // 1112, 2048 -> 1203, 4096 -> 1318, 8192 -> 1533)
+      const uint32_t wcap = pw->wide_grid ? std::max(64u, pw->wide_grid) : 512u;
       const dim3 gm(std::min<uint32_t>(groups, wcap));
       // stamped as one span: the screen (start) and the fix-up of its close calls (end)
       KTime k1 = kt;
       k1.fold = -1;
       k_project_mfma_wide<<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h,
                                                          key_or, project_eps(r.d), *pw, kt);
-      static const uint32_t fcap = [] {  // (KLSH_FIX_GRID: A/B of the fix-up launch size)
-        const char* e = getenv("KLSH_FIX_GRID");
-        return e ? (uint32_t)std::max(16, atoi(e)) : 1024u;
-      }();
+      const uint32_t fcap = pw->fix_grid ? std::max(16u, pw->fix_grid) : 1024u;  // "fix_grid"
       k_project_fix<<<fcap, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
-      return;
+      return kPkWide;
     }
   }
-  if (h16_ok(r, pw) && h > 0 && !project_mfma_requested()) {
+  if (h16_ok(r, pw) && h > 0) {
     launch_h16(r, slots, keys, n, W, h, key_or, s, *pw, kt, nullptr, nullptr);
-    return;
-  }
-  if (project_mfma_requested() && (r.d == 16 || r.d == 32 || r.d == 64)) {
-    const uint32_t groups = (n + 127) / 128;  // 4 waves x 32 rows per workgroup per step
-    const dim3 gm(std::min<uint32_t>(groups, 8192u));
-    const float eps = project_eps(r.d);
-    auto go = [&](auto kern) {  // (diagnostic variant: not stamped)
-      kern<<<gm, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, eps);
-    };
-    if (r.d == 64) go(k_project_mfma<64>);
-    else if (r.d == 32) go(k_project_mfma<32>);
-    else go(k_project_mfma<16>);
-    return;
+    return kPkH16;
   }
   auto go_pk = [&](auto kern) {
     kern<<<grid, block, 0, s>>>(r.x, r.dp, slots, keys, n, W, h, key_or, nullptr, kt, nullptr);
@@ -978,6 +836,7 @@ void launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32
       }
     }
   }
+  return kPkPacked;
 }
 
 // Stable compaction of the live slots (merge_abundance's concatenation, cluster.cc:39-45) in two
@@ -1032,12 +891,6 @@ __device__ __forceinline__ void collect_run_counts(Counters* ctr, RunCounters* r
   }
   ctr->n_huge_rows = rc->n_huge_rows.v;
   rc->n_huge_rows.v = 0u;
-#pragma unroll
-  for (int c = 0; c < kGroupClasses; ++c) rc->n_act[c].v = 0u;
-  ctr->n_act_rows = rc->n_act_rows.v;
-  rc->n_act_rows.v = 0u;
-  ctr->screened = rc->screened.v;
-  rc->screened.v = 0u;
 }
 
 // Publish the iteration's counters to the host (see Publish), `total` filled in.

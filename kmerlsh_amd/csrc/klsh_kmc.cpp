@@ -341,7 +341,10 @@ extern "C" int klsh_build_khtable(klsh_ctx* ctx, const char* const* kmc_names, i
   if (!ctx || !kmc_names || n_samples <= 0) return set_error(KLSH_E_ARG, "bad argument");
   if (k < 1 || k > 32) return set_error(KLSH_E_RANGE, "k must be in [1, 32] (Kmer::MAX_K)");
   const double t_start = now_ms();
+  if (st && st->struct_size != sizeof(klsh_khtable_stats))
+    return set_error(KLSH_E_ARG, "klsh_khtable_stats.struct_size != sizeof: built against another klsh.h");
   klsh_khtable_stats local{};
+  local.struct_size = sizeof(local);
   std::vector<KmcDb> dbs(n_samples);
   uint64_t records = 0;
   for (int j = 0; j < n_samples; ++j) {

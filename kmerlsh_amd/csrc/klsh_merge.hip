@@ -491,22 +491,18 @@ __device__ __forceinline__ void pair_batch(const uint2* __restrict__ list, uint3
 }
 
 // One wave's share of the small-run batches: waves `wave`, `wave + nwaves`, ... of the batch
-// space; lds = this wave's 64 * (D + 4) floats.  WHICH: 0 = every class, 1 = the pairs only,
-// 2 = runs of 3..64 rows only.
-template <int D, int WHICH = 0>
+// space; lds = this wave's 64 * (D + 4) floats.
+template <int D>
 __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restrict__ slots,
                                            const Decider& dc, const Rows& r, Counters* ctr,
                                            float* lds, uint32_t wave, uint32_t nwaves) {
   constexpr int NC = kGroupClasses;
   uint32_t n[NC], nb[NC], start[NC + 1];
-  // after the fp16 screen: only the runs it could not rule out (the others merge nothing)
-  const CountLine* counts = w.screened ? w.rc->n_act : w.rc->n_cls;
-  const uint2* const* lists = w.screened ? w.act : w.cls;
+  const CountLine* counts = w.rc->n_cls;
+  const uint2* const* lists = w.cls;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
-    n[c] = (WHICH == 1 && c > 0) || (WHICH == 2 && c == 0)
-               ? 0u
-               : __hip_atomic_load(&counts[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    n[c] = __hip_atomic_load(&counts[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   nb[0] = (n[0] + 63u) / 64u;
   nb[1] = batches_of<4>(n[1]);
   nb[2] = batches_of<8>(n[2]);
@@ -541,7 +537,7 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
     int c;
     uint32_t bi;
     locate(t, c, bi);
-    if (WHICH == 1 || c == 0) return;  // pairs load their own
+    if (c == 0) return;  // pairs load their own
     const uint32_t G = 2u << c, NG = 64u / G;
     const uint32_t k = bi * NG + lane / G, g = lane & (G - 1);
     if (k < n[c]) {
@@ -559,18 +555,12 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
     int c;
     uint32_t bi;
     locate(t, c, bi);
-    if constexpr (WHICH == 1) {
-      pair_batch<D>(lists[0], n[0], bi, slots, dc, r, ctr, w.dlist);
-      continue;
-    }
 #ifdef KLSH_SMALL_RT_G
-    if (WHICH != 2 && c == 0) pair_batch<D>(lists[0], n[0], bi, slots, dc, r, ctr, w.dlist);
+    if (c == 0) pair_batch<D>(lists[0], n[0], bi, slots, dc, r, ctr, w.dlist);
     else merge_batch<0, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr, 2u << c);
 #else
     switch (c) {  // wave-uniform
-      case 0:
-        if constexpr (WHICH != 2) pair_batch<D>(lists[0], n[0], bi, slots, dc, r, ctr, w.dlist);
-        break;
+      case 0: pair_batch<D>(lists[0], n[0], bi, slots, dc, r, ctr, w.dlist); break;
       case 1: merge_batch<4, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
       case 2: merge_batch<8, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
       case 3: merge_batch<16, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
@@ -584,231 +574,15 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
 }
 
 
-// ------------------------------------------------- the fp16 screen of the small runs -----
-// Every run of 2..64 rows is first tested on the fp16 row image (Rows::xh, half the bytes of the
-// f32 rows): a run can merge only if some pair (a, b) passes cosine >= s*, and
-//   |x~a.x~b / (|x~a| |x~b|) - fl(dot_ref / fl(sqrtf(nrm_a) sqrtf(nrm_b)))| <= m
-// with m = screen_m0 + screen_a2 (1/|x~a| + 1/|x~b|): the fp16 rounding of both rows (2^-11 each,
-// relative, plus 2^-25 absolute per element for subnormals), the screen's f32 sums, the
-// reference's own sequential sums and the quotient's roundings, 1.5x headroom (screen_margins).
-// A run none of whose pairs reaches s* - m cannot merge (cluster.cc:66-69): it is left as it is —
-// the walk's result for it is "no change" — and only the others go on to k_merge_small (lists
-// MergeWork::act), which decides them exactly on the f32 rows.  One wave per workgroup; the
-// batches of every class (64/G runs of G lanes, lane g = position g) in one persistent space;
-// passed runs collect in LDS per class and go out 32+ at a time (one atomic per flush).
-typedef _Float16 sh16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 sh16x2 __attribute__((ext_vector_type(2)));
-typedef float pf16acc __attribute__((ext_vector_type(16)));
-typedef float pf4acc __attribute__((ext_vector_type(4)));
-
-template <int D>
-__global__ __launch_bounds__(64) void k_small_screen(MergeWork w, const uint32_t* __restrict__ slots,
-                                                     Rows r, float s_star, float m0, float a2,
-                                                     KTime kt) {
-  constexpr int NC = kGroupClasses, STH = D + 8;  // LDS row stride in halves (16-B pad)
-  __shared__ __attribute__((aligned(16))) _Float16 lrow[64 * STH];
-  __shared__ float linv[64];
-  __shared__ uint32_t lflag[64];  // per run of the batch: some pair not ruled out
-  __shared__ uint2 buf[NC][64];
-  kt_begin(kt, KC_SCREEN);
-  const uint32_t lane = __lane_id();
-  if (blockIdx.x == 0 && lane == 0) w.rc->screened.v = 1u;
-  uint32_t n[NC], nb[NC], start[NC + 1], bcnt[NC], brows[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    n[c] = __hip_atomic_load(&w.rc->n_cls[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t per = 32u >> c;  // runs per batch: 64 / G, G = 2 << c
-    nb[c] = (n[c] + per - 1u) / per;
-    bcnt[c] = brows[c] = 0u;
-  }
-  {
-    uint32_t a = 0;
-#pragma unroll
-    for (int c = NC - 1; c >= 0; --c) {
-      start[c] = a;
-      a += nb[c];
-    }
-    start[NC] = a;
-  }
-  auto flush = [&](int c) {  // this wave's passed runs of class c to the global list
-#ifdef KLSH_SCREEN_NOFLUSH  // diagnostics build only: the screen's cost without its list (wrong result)
-    bcnt[c] = brows[c] = 0u;
-    return;
-#endif
-    uint32_t base = 0;
-    if (lane == 0) {
-      base = atomicAdd(&w.rc->n_act[c].v, bcnt[c]);
-      atomicAdd(&w.rc->n_act_rows.v, brows[c]);
-    }
-    base = shfl32(base, 0);
-    wave_lds_fence();
-    if (lane < bcnt[c]) w.act[c][base + lane] = buf[c][lane];
-    wave_lds_fence();
-    bcnt[c] = brows[c] = 0u;
-  };
-  const uint64_t below = lanes_below(lane);
-  // batch t -> (class, the lane's run entry), then the lane's slot: a three-stage pipeline —
-  // this batch is screened while the next one's rows, the one after's slot and the third one's
-  // list entry are in flight, so no dependent load is waited on inside the loop
-  auto entry_of = [&](uint32_t t, int& c, uint2& e) {
-    c = 0;
-    e = make_uint2(0u, 0u);
-    if (t >= start[NC]) return;
-#pragma unroll
-    for (int q = NC - 1; q >= 0; --q)
-      if (t >= start[q] && t < start[q] + nb[q]) c = q;
-    const uint32_t G = 2u << c, NG = 64u / G;
-    const uint32_t k = (t - start[c]) * NG + lane / G;
-    if (k < n[c]) e = w.cls[c][k];
-  };
-  auto slot_of = [&](int c, const uint2& e) -> uint32_t {
-    const uint32_t g = lane & ((2u << c) - 1u);
-    return g < e.y ? slots[e.x + g] : 0u;
-  };
-  sh16x8 xr[D / 8];
-  auto load_rows = [&](uint32_t slot) {
-    const uint16_t* src = r.xh + (size_t)slot * r.dp;
-#pragma unroll
-    for (int q = 0; q < D / 8; ++q) xr[q] = *reinterpret_cast<const sh16x8*>(src + 8 * q);
-  };
-  int c, c1, c2;
-  uint2 e, e1, e2;
-  entry_of(blockIdx.x, c, e);
-  load_rows(slot_of(c, e));
-  entry_of(blockIdx.x + gridDim.x, c1, e1);
-  uint32_t slot1 = slot_of(c1, e1);
-  entry_of(blockIdx.x + 2u * gridDim.x, c2, e2);
-  for (uint32_t t = blockIdx.x; t < start[NC]; t += gridDim.x) {
-    sh16x8 own[D / 8];
-#pragma unroll
-    for (int q = 0; q < D / 8; ++q) own[q] = xr[q];
-    load_rows(slot1);                      // batch t + 1's rows
-    const uint32_t slot2 = slot_of(c2, e2);  // batch t + 2's slot
-    int c3;
-    uint2 e3;
-    entry_of(t + 3u * gridDim.x, c3, e3);  // batch t + 3's entry
-    const uint32_t G = 2u << c;
-    const uint32_t g = lane & (G - 1);
-    const uint32_t b = e.y;
-    const bool valid = g < b;
-    float ss = 0.0f;
-#pragma unroll
-    for (int q = 0; q < D / 8; ++q) {
-      *reinterpret_cast<sh16x8*>(lrow + lane * STH + 8 * q) = own[q];
-#pragma unroll
-      for (int hi2 = 0; hi2 < 8; hi2 += 2) {
-        const sh16x2 v = {own[q][hi2], own[q][hi2 + 1]};
-        ss = __builtin_amdgcn_fdot2(v, v, ss, false);
-      }
-    }
-    const float inv = 1.0f / __builtin_sqrtf(ss);  // inf for a zero row, NaN for NaN
-    linv[lane] = valid ? inv : 0.0f;  // 0: not a row of a run (never tested)
-    lflag[lane] = 0u;
-    wave_lds_fence();
-    // The Gram blocks of the batch's runs on the matrix cores (x~ . x~ exact products, f32 sums):
-    // 32 x 32 tiles for runs of 17..64 rows (the upper-triangular tiles of each run), 16 x 16
-    // diagonal tiles for shorter runs (4 per batch, runs never cross a 16-row block).  A pair
-    // (R < C) of one run that the screen cannot rule out flags the run in LDS.
-    const uint32_t lg = (uint32_t)__builtin_ctz(G);  // log2 G
-    auto test = [&](uint32_t R, uint32_t C, float sv) {
-      if (R < C && (R >> lg) == (C >> lg)) {
-        const float ir = linv[R], ic = linv[C];
-        if (ir != 0.0f && ic != 0.0f) {
-          const float qv = sv * ir * ic;
-          const float m = m0 + a2 * (ir + ic);
-          if (!(qv < s_star - m)) lflag[R >> lg] = 1u;  // NaN / inf: not ruled out
-        }
-      }
-    };
-    if constexpr (D < 32) {  // (not launched: screen_ok needs d >= 32) rule nothing out
-      lflag[lane] = 1u;
-    } else if (G >= 32u) {
-      const uint32_t r32 = lane & 31u, k8 = 8u * (lane >> 5);
-#pragma unroll 1
-      for (int tt = 0; tt < 3; ++tt) {
-        const uint32_t tr = tt == 2 ? 1u : 0u, tc = tt == 0 ? 0u : 1u;
-        if (G == 32u && tt == 1) continue;  // two runs: their diagonal tiles only
-        pf16acc acc;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          const sh16x8 fa = *reinterpret_cast<const sh16x8*>(lrow + (tr * 32u + r32) * STH + 16 * ks + k8);
-          const sh16x8 fb = *reinterpret_cast<const sh16x8*>(lrow + (tc * 32u + r32) * STH + 16 * ks + k8);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-          test(tr * 32u + (uint32_t)(q & 3) + 8u * (uint32_t)(q >> 2) + 4u * (lane >> 5),
-               tc * 32u + r32, acc[q]);
-      }
-    } else {
-      const uint32_t r16 = lane & 15u, k8 = 8u * (lane >> 4);
-#pragma unroll 1
-      for (int tb = 0; tb < 4; ++tb) {
-        pf4acc acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int ks = 0; ks < D / 32; ++ks) {
-          const sh16x8 f = *reinterpret_cast<const sh16x8*>(lrow + (16u * tb + r16) * STH + 32 * ks + k8);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(f, f, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          test(16u * tb + 4u * (lane >> 4) + (uint32_t)q, 16u * tb + r16, acc[q]);
-      }
-    }
-    wave_lds_fence();
-    const bool grp = lflag[lane >> lg] != 0u;
-    const bool leader = g == 0u && b >= 2u && grp;
-    const uint64_t lead = __ballot(leader);
-    if (lead) {  // (c is wave-uniform)
-      if (leader) buf[c][bcnt[c] + (uint32_t)__popcll(lead & below)] = e;
-      uint32_t rsum = leader ? b : 0u;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) rsum += (uint32_t)__shfl_xor((int)rsum, o, 64);
-      bcnt[c] += (uint32_t)__popcll(lead);
-      brows[c] += rsum;
-      if (bcnt[c] > 32u) flush(c);
-    }
-    wave_lds_fence();  // the rows of this batch are read before the next batch overwrites them
-    c = c1;
-    e = e1;
-    c1 = c2;
-    e1 = e2;
-    slot1 = slot2;
-    c2 = c3;
-    e2 = e3;
-  }
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-    if (bcnt[c]) flush(c);
-  kt_end(kt, KC_SCREEN);
-}
-
-#ifdef KLSH_SPLIT_PAIRS
-constexpr int kSmallWhich = 2;  // runs of 3..64 rows here, the pairs in k_merge_pairs
-#else
-constexpr int kSmallWhich = 0;
-#endif
 template <int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_merge_small(
     MergeWork w, uint32_t* __restrict__ slots,
                                                     Decider dc, Rows r, Counters* ctr) {
   __shared__ __attribute__((aligned(16))) float lds[64 * (D + 4)];
   kt_begin(w.kt, KC_SMALL);
-  small_loop<D, kSmallWhich>(w, slots, dc, r, ctr, lds, blockIdx.x, gridDim.x);
+  small_loop<D>(w, slots, dc, r, ctr, lds, blockIdx.x, gridDim.x);
   kt_end(w.kt, KC_SMALL);
 }
-#ifdef KLSH_SPLIT_PAIRS
-// The runs of exactly 2 rows alone: no LDS and fewer registers, so three waves per SIMD.
-template <int D>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_merge_pairs(
-    MergeWork w, uint32_t* __restrict__ slots, Decider dc, Rows r, Counters* ctr) {
-  kt_begin(w.kt, KC_PAIRS);
-  small_loop<D, 1>(w, slots, dc, r, ctr, nullptr, blockIdx.x, gridDim.x);
-  kt_end(w.kt, KC_PAIRS);
-}
-#endif
 
 // Runs of equal keys, listed by size class, in three launches and no contended atomics:
 //   k_runs_count  a tile of 4096 positions is read coalesced (position k*256 + t by thread t), its
@@ -2568,35 +2342,9 @@ struct Fork {
   }
 };
 
-// The small-run screen's margin (k_small_screen): |q~ - q_ref| <= m0 + a2 (1/|x~a| + 1/|x~b|) for
-// the screen's quotient q~ = x~a.x~b / (|x~a| |x~b|) against the reference's fl(dot / den):
-//   m0: fp16 rounding of both rows in the dot (2 * 2^-11) and in the two norms (2 * 2^-11),
-//       2^-20 for the products of the rounding errors, (4d + 16) 2^-24 for the f32 sums of the
-//       screen and of the reference (dot, |a|^2, |b|^2) and the sqrt / product / quotient roundings
-//   a2: 2^-25 per element absolute (fp16 subnormals, which gfx950 keeps in the conversion, the
-//       MFMA and v_dot2_f32_f16 under the default float mode: tools/denorm_probe.hip), summed with
-//       Cauchy-Schwarz: sqrt(d) 2^-25 (|a| + |b|) / (|a||b|), doubled (the norms' own share)
-// all times 1.5 for headroom.  Only with a fast decider (a normal s*) and the fp16 image.
-static void screen_margins(int d, float* m0, float* a2) {
-  *m0 = 1.5f * (0x1p-9f + 0x1p-20f + (4.0f * (float)d + 16.0f) * 0x1p-24f);
-  *a2 = 1.5f * 2.0f * 0x1p-25f * std::sqrt((float)d);
-}
-static bool screen_ok(const Rows& r, const Decider& dc) {
-  // off by default: measured neutral on C2 (the screen's per-wave list flushes)
-  static const bool on = [] {
-    const char* e = getenv("KLSH_SMALL_SCREEN");
-    return e && atoi(e) != 0;
-  }();
-  return on && r.xh && dc.fast && (r.d == 32 || r.d == 64);  // (16x16x32 tiles: d >= 32)
-}
-
-// The small-run merge's persistent launch (KLSH_SMALL_GRID: A/B of its size; default 12288).
-static uint32_t small_grid() {
-  static const uint32_t g = [] {
-    const char* e = getenv("KLSH_SMALL_GRID");
-    return e ? (uint32_t)std::max(256, atoi(e)) : 12288u;
-  }();
-  return g;
+// The small-run merge's persistent launch (option "small_grid"; default 12288).
+static uint32_t small_grid(const MergeWork& w) {
+  return w.small_grid ? std::max(256u, w.small_grid) : 12288u;
 }
 
 // Iterations below this many positions run every merge class in ONE launch (k_merge_tail) on the
@@ -2618,14 +2366,10 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_tail<D>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess;
     (void)lds_ok;
-    static const uint32_t nbig = [] {  // (KLSH_TAIL_NBIG / KLSH_TAIL_NSMALL: A/B of the split)
-      const char* e = getenv("KLSH_TAIL_NBIG");
-      return e ? (uint32_t)std::max(1, atoi(e)) : 128u;  // 32 / 64 / 128 / 256 swept
-    }();
-    static const uint32_t nsmall = [] {
-      const char* e = getenv("KLSH_TAIL_NSMALL");
-      return e ? (uint32_t)std::max(1, atoi(e)) : 512u;  // 128 / 256 / 512 / 1024 swept
-    }();
+    // options "tail_big_groups" / "tail_small_groups": 32 / 64 / 128 / 256 and 128 / 256 / 512 /
+    // 1024 swept (round 3)
+    const uint32_t nbig = w.tail_nbig ? w.tail_nbig : 128u;
+    const uint32_t nsmall = w.tail_nsmall ? w.tail_nsmall : 512u;
     k_merge_tail<D><<<nbig + nsmall, 256, lds, s>>>(w, slots, dc, r, ctr, nbig);
     return;
   }
@@ -2651,28 +2395,8 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   // retire and re-enter as the big-run workgroups come and go (C2, same box, interleaved:
   // 4608 -> 255.9 / 258.0 ms, 8192 -> 255.4 / 252.3, 12288 -> 250.8 / 251.7, 16384 -> 256.0 /
   // 253.9; small-run merge 79.4 -> 70.5 ms per step)
-#ifdef KLSH_SPLIT_PAIRS
-  static const int pairs_lane = getenv("KLSH_PAIRS_MAIN") ? 3 : 2;
-  k_merge_pairs<D><<<12288, 64, 0, pairs_lane == 3 ? s : f.lane(2)>>>(w, slots, dc, r, ctr);
-#endif
-  // the fp16 screen first (where the row image exists): the merge then takes only the runs it
-  // could not rule out
-  if (screen_ok(r, dc)) {
-    float m0, a2;
-    screen_margins(r.d, &m0, &a2);
-    static const uint32_t sgrid = [] {  // (KLSH_SCREEN_GRID: A/B of the launch size)
-      const char* e = getenv("KLSH_SCREEN_GRID");
-      return e ? (uint32_t)std::max(64, atoi(e)) : 2048u;  // 512..4096 swept: 2048 best
-    }();
-    k_small_screen<D><<<sgrid, 64, 0, f.lane(2)>>>(w, slots, r, dc.s_star, m0, a2, w.kt);
-    MergeWork ws = w;
-    ws.screened = 1u;
-    if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
-    k_merge_small<D><<<small_grid(), 64, 0, f.lane(2)>>>(ws, slots, dc, r, ctr);
-  } else {
-    if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
-    k_merge_small<D><<<small_grid(), 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
-  }
+  if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
+  k_merge_small<D><<<small_grid(w), 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
   if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[1], f.lane(2));
 }
 
@@ -2697,11 +2421,9 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
   auto grid = [&](int c, uint32_t per_wave) {
     // up to 8192 one-wave workgroups per class (was 2048: C5 2.58 / 2.55 -> 2.36 / 2.33 s per
     // step, interleaved on one box), as for the register-row small-run launch
-    static const uint64_t cap = [] {  // (KLSH_WIDE_GROUP_GRID: A/B of the launch size)
-      const char* e = getenv("KLSH_WIDE_GROUP_GRID");
-      // 4096 -> 1221, 8192 -> 1141, 16384 -> 1103, 32768 -> 1102 ms per C5 step (one box)
-      return e ? (uint64_t)std::max(64, atoi(e)) : 16384ull;
-    }();
+    // option "wide_group_grid": 4096 -> 1221, 8192 -> 1141, 16384 -> 1103, 32768 -> 1102 ms
+    // per C5 step (one box)
+    const uint64_t cap = w.wide_group_grid ? std::max(64u, w.wide_group_grid) : 16384u;
     return (uint32_t)std::min<uint64_t>(cap, group_class_capacity(c, n) / per_wave + 1);
   };
   const Fork f(w, s);

@@ -92,56 +92,131 @@ def test_hash_keys_random_vs_oracle(engine, oracle):
         assert np.array_equal(engine.hash_keys(rows, w), oracle.keys(rows, w)), (d, h)
 
 
-def test_hash_keys_close_calls_vs_oracle(engine, oracle):
-    """Rows on (or within float noise of) hyperplanes: the matrix-core screen cannot call these
-    signs, the exact sequential chain must (s == +0/-0 -> 1, tiny negative -> 0, NaN -> 0); plus
-    tiny, huge, zero and NaN rows."""
+def adversarial_rows(rng, n, d, w):
+    """Rows the certified projection screens cannot call, and rows that break the fp16 image:
+    every third row projected onto hyperplane i % h (s is rounding noise around 0), rows whose
+    sequential sum is exactly 0 for a hyperplane (x = w_l e_k - w_k e_l: the two products are
+    exact negatives), zero / -0 / tiny / huge / NaN / inf rows, elements past fp16's range
+    (>= 65520 -> inf in the image), fp16-subnormal rows and rows whose fp16 image is all zero
+    while the f32 row is not, f32-subnormal rows."""
+    h = w.shape[0]
+    w64 = w.astype(np.float64)
+    rows = rng.normal(0, 1, size=(n, d))
+    for i in range(0, n, 3):
+        j = i % h
+        rows[i] -= (rows[i] @ w64[j]) / (w64[j] @ w64[j]) * w64[j]
+    rows = rows.astype(np.float32)
+    f = np.float32
+    rows[1] = 0.0
+    rows[4] *= f(1e-30)
+    rows[7] *= f(1e30)
+    rows[10, 3] = np.nan
+    rows[13] = -0.0
+    for m, i in enumerate(range(2, min(n, 2 + 3 * h * 4), 3)):  # s == 0 exactly for hyperplane j
+        j, k = m % h, (m * 7) % d
+        l = (k + 1 + m % (d - 1)) % d if d > 1 else k
+        if l == k:
+            continue
+        rows[i] = 0.0
+        rows[i, k], rows[i, l] = w[j, l], -w[j, k]
+        if m % 2:
+            rows[i] *= f(-1)
+    special = {
+        16: lambda r: r.__setitem__(0, f(70000.0)),      # fp16 overflow: inf in the image
+        19: lambda r: r.__setitem__(d - 1, f(65519.0)),  # rounds to 65504, finite
+        22: lambda r: r.__imul__(f(1e-6)),               # fp16 subnormal image
+        25: lambda r: r.__imul__(f(1e-9)),               # fp16 image all zero, f32 nonzero
+        28: lambda r: r.__setitem__(slice(0, d // 2), r[: d // 2] * f(1e-9)),
+        31: lambda r: r.__setitem__(slice(None), np.where(np.arange(d) % 2, f(-0.0), f(0.0))),
+        34: lambda r: r.__setitem__(0, f(np.inf)),
+        37: lambda r: r.__imul__(f(1e-40)),              # f32 subnormal
+        40: lambda r: r.__setitem__(slice(None), f(65504.0)),
+        43: lambda r: r.__setitem__(d // 2, f(-1e5)),
+    }
+    for i, fn in special.items():
+        if i < n:
+            fn(rows[i])
+    return rows
+
+
+@pytest.mark.parametrize("d,h", [(64, 23), (32, 18), (16, 9), (64, 31), (32, 1), (8, 7),
+                                 (512, 20), (100, 31), (72, 5)])
+def test_hash_keys_close_calls_vs_oracle(engine, oracle, d, h):
+    """The loop's projection kernels (klsh_hash_keys uses the same dispatch and, at d = 16/32/64,
+    the fp16 row image) on adversarial rows, bit-equal to the reference's sequential chains
+    (hash/lshash.cc:44-59: s == +0/-0 -> 1, tiny negative -> 0, NaN -> 0).  The screen runs and
+    leaves close calls to the exact chains, which the test asserts."""
     from kmerlsh_amd import _native
 
-    rng = np.random.default_rng(11)
-    for d, h in [(64, 23), (32, 18), (16, 9), (512, 20), (100, 31), (72, 5)]:
-        w, _ = _native.hyperplanes(7 + d, 0, h, d)
-        w64 = w.astype(np.float64)
-        rows = rng.normal(0, 1, size=(4000, d))
-        for i in range(0, 4000, 3):  # project out hyperplane i % h: s is rounding noise around 0
-            j = i % h
-            rows[i] -= (rows[i] @ w64[j]) / (w64[j] @ w64[j]) * w64[j]
-        rows = rows.astype(np.float32)
-        rows[1] = 0.0
-        rows[4] *= np.float32(1e-30)
-        rows[7] *= np.float32(1e30)
-        rows[10, 3] = np.nan
-        rows[13] = -0.0
-        got = engine.hash_keys(rows, w)
-        assert np.array_equal(got, oracle.keys(rows, w)), (d, h)
+    rng = np.random.default_rng(11 + d + h)
+    w, _ = _native.hyperplanes(7 + d, 0, h, d)
+    rows = adversarial_rows(rng, 4000, d, w)
+    got = engine.hash_keys(rows, w)
+    assert np.array_equal(got, oracle.keys(rows, w)), (d, h)
+    kern = engine.get_option("last_hash_kernel")
+    assert kern == {16: 1, 32: 1, 64: 1, 8: 0}.get(d, 2), kern  # fp16 screen / packed / bf16x3
+    if kern:
+        assert engine.get_option("last_hash_close_pairs") > 0
 
 
-def test_hash_keys_matrix_core_variant():
-    """The certified matrix-core projection (KLSH_PROJECT=mfma) on the same close calls, in a
-    child process (the kernel variant is chosen once per process)."""
-    code = (
-        "import sys; sys.path[:0] = [%r, %r]\n"
-        "import numpy as np, klsh_oracle as oracle\n"
-        "from kmerlsh_amd import _native\n"
-        "rng = np.random.default_rng(11)\n"
-        "with _native.Engine(0) as eng:\n"
-        "  for d, h in [(64, 23), (32, 31), (16, 9)]:\n"
-        "    w, _ = _native.hyperplanes(7 + d, 0, h, d)\n"
-        "    w64 = w.astype(np.float64)\n"
-        "    rows = rng.normal(0, 1, size=(5000, d))\n"
-        "    for i in range(0, 5000, 3):\n"
-        "      j = i %% h\n"
-        "      rows[i] -= (rows[i] @ w64[j]) / (w64[j] @ w64[j]) * w64[j]\n"
-        "    rows = rows.astype(np.float32)\n"
-        "    rows[1] = 0.0; rows[4] *= np.float32(1e-30); rows[7] *= np.float32(1e30)\n"
-        "    rows[10, 3] = np.nan; rows[13] = -0.0\n"
-        "    assert np.array_equal(eng.hash_keys(rows, w), oracle.keys(rows, w)), (d, h)\n"
-        "print('ok')\n"
-    ) % (ROOT, os.path.join(ROOT, "oracle"))
-    env = dict(os.environ, KLSH_PROJECT="mfma")
-    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
-                         timeout=120)
-    assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-2000:]
+@pytest.mark.parametrize("segcap", [1, 3])
+def test_hash_keys_fp16_fixup_segment_full(engine, oracle, segcap):
+    """k_project_h16's fix-up segment filled up (a test-only cap of 1 or 3 entries per workgroup):
+    the close calls past it are settled in place by the exact chain, same bits."""
+    from kmerlsh_amd import _native
+
+    engine.set_option("h16_segcap", segcap)
+    try:
+        for d, h in [(64, 23), (32, 17), (16, 12)]:
+            w, _ = _native.hyperplanes(3 + d, 0, h, d)
+            rows = adversarial_rows(np.random.default_rng(d), 9000, d, w)
+            assert np.array_equal(engine.hash_keys(rows, w), oracle.keys(rows, w)), (d, h)
+            assert engine.get_option("last_hash_kernel") == 1
+    finally:
+        engine.set_option("h16_segcap", 0)
+
+
+def test_hash_keys_packed_variant(engine, oracle):
+    """Option "projection" = 1: the exact packed VALU chains at every width, the same keys."""
+    from kmerlsh_amd import _native
+
+    engine.set_option("projection", 1)
+    try:
+        for d, h in [(64, 23), (32, 31), (16, 9), (100, 20)]:
+            w, _ = _native.hyperplanes(7 + d, 0, h, d)
+            rows = adversarial_rows(np.random.default_rng(d), 5000, d, w)
+            assert np.array_equal(engine.hash_keys(rows, w), oracle.keys(rows, w)), (d, h)
+            assert engine.get_option("last_hash_kernel") == 0
+    finally:
+        engine.set_option("projection", 0)
+
+
+@pytest.mark.parametrize("d", [64, 32])
+def test_cluster_variants_agree(engine, oracle, d):
+    """Options that change the launch sequence, not the result: the queued tail batches
+    ("tail_batch") and the fp16-image projection ("projection") in all four combinations give the
+    same N_t trace, RNG counter, statistics that count work, and result bits as the oracle."""
+    rng = np.random.default_rng(d + 1)
+    rows = clustered(rng, 120000, d, 1500, 0.05)
+    want = oracle.cluster(rows, 0.8, 14, 1000000, 91, 2)
+    seen = []
+    try:
+        for tail_batch in (1, 0):
+            for proj in (0, 1):
+                engine.set_option("tail_batch", tail_batch)
+                engine.set_option("projection", proj)
+                engine.load_rows(rows)
+                assert engine.get_option("fp16_image") == (proj == 0)
+                trace, counter, st = engine.cluster(0.8, 14, 1000000, 91, 2)
+                assert np.array_equal(trace, want[3]) and counter == want[4], (tail_batch, proj)
+                assert_same_result(engine.result(), *want[:3])
+                assert st["project_launches"] == st["iterations"] == 14
+                seen.append((st["iterations"], st["sum_merges"], st["hyperplanes"],
+                             st["sum_rows"], st["sum_proj_bits"]))
+    finally:
+        engine.set_option("tail_batch", 1)
+        engine.set_option("projection", 0)
+    assert len(set(seen)) == 1, seen
 
 
 # ------------------------------------------------------------------------------ p_cluster ---
