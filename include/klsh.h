@@ -156,6 +156,8 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *   "phase_timing"     0/1: per-phase HIP events (adds latency; default 0)
  *   "kernel_timing"    0/1: the per-class statistics of klsh_stats.kern (default 1)
  *   "tail_batch"       0/1: queue the small late iterations 32 at a time (default 1)
+ *   "huge_fold"        1 (tests): runs over 896 rows always walked inside the 385..896-row
+ *                      kernel (default 0: only after several iterations without such runs)
  *   "projection"       0 = the certified matrix-core screens where they exist (default: the fp16
  *                      row image at d = 16, 32, 64 — kept beside the rows, 2 bytes per value —
  *                      and bf16x3 above 64), 1 = the exact packed VALU chains only (no fp16 image)

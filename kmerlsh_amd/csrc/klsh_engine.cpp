@@ -203,6 +203,8 @@ struct klsh_ctx {
   // canonical order and runs the remaining iterations on its replica — identically, with no
   // communication.  klsh_set_option(ctx, "shard_min_rows", n); 0 = always sharded.
   uint64_t shard_min_rows = 1u << 21;
+  uint32_t huge_quiet = 0;  // consecutive iterations without >896-row runs (MergeWork::huge_fold)
+  bool huge_fold_always = false;  // option "huge_fold" (tests): fold in every iteration
   // option "comm_timeout_s": a collective that has not completed after this long aborts the group
   double comm_timeout_s = 600.0;
 
@@ -983,6 +985,10 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
   // iterations without them between ones with dozens: a cap of 4 serialised those walks,
   // k_merge_huge<32> 746 -> 1024 ms per step)
   ctx->mw.huge_cap = ctx->h_ctr->n_huge == 0 ? 64u : 0u;
+  // several iterations in a row without them: the next one walks any >896-row runs inside the
+  // 385..896-row kernel instead of launching k_merge_huge (an empty launch on C2 / C5)
+  ctx->huge_quiet = ctx->h_ctr->n_huge == 0 ? ctx->huge_quiet + 1 : 0;
+  ctx->mw.huge_fold = (ctx->huge_quiet >= 4 || ctx->huge_fold_always) ? 1u : 0u;
   if (ctx->h_ctr->n_over > 0) {
     std::vector<uint2> over;
     uint64_t hyp = 0;
@@ -1576,6 +1582,8 @@ int klsh_cluster(klsh_ctx* ctx, float min_similarity, int iterations, int bucket
   st->struct_size = sizeof(*st);
   st->world = (uint64_t)ctx->world();
   ctx->mw.huge_cap = 0;  // (set per iteration from the run counts by the single-device loop)
+  ctx->mw.huge_fold = ctx->huge_fold_always ? 1u : 0u;
+  ctx->huge_quiet = 0;
   ctx->mw.dlist = nullptr;
   const int run_iters = ctx->stop_after > 0 ? std::min(iterations, ctx->stop_after) : iterations;
   if (ctx->comm)  // any bound group, world 1 included (measures the sharded machinery alone)
@@ -1689,6 +1697,7 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   if (n == "phase_timing") return flag(&ctx->phase_timing);
   if (n == "kernel_timing") return flag(&ctx->kernel_timing);
   if (n == "tail_batch") return flag(&ctx->tail_batch);
+  if (n == "huge_fold") return flag(&ctx->huge_fold_always);
   if (n == "hyperplane_window") {
     if (value < 0) return fail(KLSH_E_ARG, "hyperplane_window must be >= 0");
     ctx->hyperplane_window = (uint64_t)value;
@@ -1730,6 +1739,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "phase_timing") *value = ctx->phase_timing;
   else if (n == "kernel_timing") *value = ctx->kernel_timing;
   else if (n == "tail_batch") *value = ctx->tail_batch;
+  else if (n == "huge_fold") *value = ctx->huge_fold_always;
   else if (n == "hyperplane_window") *value = (int64_t)ctx->hyperplane_window;
   else if (n == "stop_after") *value = ctx->stop_after;
   else if (n == "projection") *value = ctx->pw.variant;
@@ -1943,6 +1953,8 @@ int klsh_pcluster(klsh_ctx* ctx, float thr) {
   if (n == 0) return 0;
   hipStream_t s = ctx->stream;
   if (int e = ctx->reset_counters()) return e;
+  ctx->mw.huge_fold = ctx->huge_fold_always ? 1u : 0u;
+  ctx->mw.huge_cap = 0;
   KLSH_HIP(hipMemsetAsync(ctx->keys, 0, 4ull * n, s));  // one bucket: every key equal
   uint64_t dummy = 0;
   if (int e = merge_and_compact(ctx, ctx->keys, ctx->order, n, thr, -1, 0, &dummy, nullptr, false))

@@ -135,6 +135,10 @@ struct MergeWork {
   // engine sets a cap of 64 after an iteration without such runs: an empty launch of hundreds of
   // 512-lane workgroups waits for CUs behind the other classes (C2: 25 ms per step of span)
   uint32_t huge_cap;
+  // 1: no k_merge_huge launch; the 385..896-row kernel's workgroups walk the >896-row list after
+  // their own (set after several iterations without such runs: C2 and C5 never have any, and an
+  // empty launch still costs its dispatch; C4, where they recur, keeps the 512-lane kernel)
+  uint32_t huge_fold;
   // launch sizes (klsh_set_option; 0 = the measured default, see the launch code)
   uint32_t small_grid;       // "small_grid": the small-run merge's persistent launch
   uint32_t tail_nbig;        // "tail_big_groups": k_merge_tail's big-run workgroups
@@ -184,7 +188,7 @@ struct Decider {
 };
 // |G - dot| <= 5.4e-5 * |a| |b| for the bf16x3 Gram value at d <= 64 (split residuals
 // 3.03 * 2^-16, the MFMA sum <= 29 chained f32 adds per term at 2u, the reference's own 65u; see
-// project_eps) against the reference's sequential f32 dot; the margin adds headroom for den's
+// the wide-row projection's bound) against the reference's sequential f32 dot; the margin adds headroom for den's
 // rounding and the approximate quotient.
 constexpr float kGramMargin = 1.0e-4f;
 Decider make_decider(float thr);

@@ -294,33 +294,7 @@ __global__ __launch_bounds__(256) void k_project_generic(const float* __restrict
   kt_end(kt, KC_PROJECT);
 }
 
-// Matrix-core projection of f32 rows (wide rows, k_project_mfma_wide below), certified: S = X W^T
-// with the bf16x3 split (x = hi + lo; hi.hi + hi.lo + lo.hi, f32 accumulation) on
-// v_mfma_f32_32x32x16_bf16.  |S - s| <= eps * |w| |x| against the reference's sequential f32 sum
-// s (eps from project_eps(d)), so every sign with |S| > eps |w| |x| is the reference's bit; the
-// rest (and any NaN, tiny or huge row) take the exact sequential chain.
-typedef __bf16 pbf16x8 __attribute__((ext_vector_type(8)));
 typedef float pf32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ void psplit8(float4 u, float4 v, pbf16x8& hi, pbf16x8& lo) {
-  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 hb = (__bf16)x[j];
-    hi[j] = hb;
-    lo[j] = (__bf16)(x[j] - (float)hb);  // exact in f32
-  }
-}
-
-float project_eps(int d) {
-  // |S - s| / (|w| |x|) <= 3.03 * 2^-16          split residuals and the dropped lo.lo term
-  //                      + (16 + 3 ceil(d/16) + 1) * 2^-23   the MFMA sum: each term passes through
-  //                        at most 16 internal adds + one per chained MFMA (counted at 2u)
-  //                      + (d + 1) * 2^-24        the reference's own sequential sum
-  // times 1.5 for headroom
-  const float ks = (float)((d + 15) / 16);
-  return 1.5f * (3.03f * 0x1p-16f + (17.0f + 3.0f * ks) * 0x1p-23f + (float)(d + 1) * 0x1p-24f);
-}
 
 // The projection from the fp16 row image (Rows::xh), certified.  x~ = fp16(x) is read (2d bytes a
 // row, half the f32 row gather) and S = x~ . w is taken on v_mfma_f32_32x32x16_f16 with w split
@@ -531,26 +505,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   kt_end(kt, KC_PROJECT);
 }
 
-// Wide rows (d > 64, any d): the same certified matrix-core screen with the hyperplanes pre-split
-// into bf16 hi/lo fragments in LDS ([k-step][lane] 32 B each: 64 KB at d = 512) and the row
-// streamed 64 columns at a time (8 loads in flight per lane).  The pairs the screen cannot call
-// (≈1 % at d = 512: the bound grows with d) go to a list that k_project_fix settles with the exact
-// sequential chains afterwards, one lane per pair — in-wave they would stall 31 other rows.
-// Six waves per workgroup: the 64-KB fragment table is shared by 6 waves instead of 4, so two
-// workgroups per CU keep 12 waves (3 per SIMD at 144 VGPRs) of row loads in flight, not 8.
+// Wide rows (d > 64, any d): a certified matrix-core screen with an fp16x3 split — x = xh + xl,
+// w = wh + wl (xh = fp16(x), xl = fp16(x - xh): 22 bits of the f32 value), S = xh.wh + xh.wl +
+// xl.wh on v_mfma_f32_32x32x16_f16 — and a bound that scales with T = sum_k |x_k||w_k| (a fourth
+// MFMA, |xh|.|wh|), not with |x||w|.  Against the reference's sequential f32 sum s
+// (hash/lshash.cc:44-51):
+//   |S - s| <= eps_w T + abs_w (|w| + |x|)
+//     eps_w: split residuals and the dropped xl.wl (3 * 2^-22), the MFMA's f32 sums ((17 + 3 ceil(d/16))
+//            * 2^-23 of the summed magnitudes), the reference's own ((d + 1) * 2^-24), x 1.5
+//     abs_w: fp16 subnormals (2^-25 per element, both operands, Cauchy-Schwarz: sqrt(d) 2^-25), x 3
+// with T taken as the computed |xh|.|wh| MFMA x (1 + 2^-9) (>= sum |x_k||w_k|: fp16 rounding of
+// both operands, the MFMA's own sums of positive terms).  Against round 3's bf16x3 split and
+// eps |w||x| bound this leaves a few times fewer close calls at d = 512 (both the 2^-16 split term
+// and the Cauchy-Schwarz slack are gone).  An element past fp16's range (|x| >= 65520: inf in xh),
+// NaN or inf makes S or T non-finite, and the pair goes to the exact chain.  The hyperplane
+// fragments are pre-split in LDS ([k-step][lane] hi, lo: 64 KB at d = 512) and the row streamed 64
+// columns per round (8 loads in flight per lane).  The pairs the screen cannot call go to a list
+// that k_project_fix settles with the exact sequential chains afterwards, one lane per pair —
+// in-wave they would stall 31 other rows.  Six waves per workgroup: the 64-KB fragment table is
+// shared by 6 waves instead of 4, so two workgroups per CU keep 12 waves (3 per SIMD) of row loads
+// in flight, not 8.
+typedef _Float16 wh16x8 __attribute__((ext_vector_type(8)));
 constexpr int kWideNT = 384;
+
+float wide_eps(int d) {
+  const float ks = (float)((d + 15) / 16);
+  return 1.5f * (3.0f * 0x1p-22f + (17.0f + 3.0f * ks) * 0x1p-23f + (float)(d + 1) * 0x1p-24f);
+}
+float wide_abs(int d) { return 3.0f * 0x1p-25f * std::sqrt((float)d); }
+
+__device__ __forceinline__ void hsplit8(float4 u, float4 v, wh16x8& hi, wh16x8& lo, wh16x8& ah) {
+  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 hb = (_Float16)x[j];
+    hi[j] = hb;
+    lo[j] = (_Float16)(x[j] - (float)hb);  // x - hi is exact in f32 (finite hi)
+    ah[j] = __builtin_fabsf16(hb);
+  }
+}
+
 __global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __restrict__ X, int d, int dp,
                                                            const uint32_t* __restrict__ slots,
                                                            uint32_t* __restrict__ keys, uint32_t n,
                                                            const float* __restrict__ W, int h,
-                                                           uint32_t key_or, float eps, ProjectWork pw,
-                                                           KTime kt) {
+                                                           uint32_t key_or, float eps, float abs_c,
+                                                           ProjectWork pw, KTime kt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
   kt_fold(kt);
   kt_begin(kt, KC_PROJECT);
   const int KS = (d + 15) / 16;
-  pbf16x8* bfr = reinterpret_cast<pbf16x8*>(psm);  // [KS][64 lanes][hi, lo]
-  float* swn = reinterpret_cast<float*>(psm + (size_t)KS * 64 * 2 * sizeof(pbf16x8));  // [32]
+  wh16x8* bfr = reinterpret_cast<wh16x8*>(psm);  // [KS][64 lanes][hi, lo]
+  float* swn = reinterpret_cast<float*>(psm + (size_t)KS * 64 * 2 * sizeof(wh16x8));  // [32]
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, r = lane & 31u, hh = lane >> 5;
   // hyperplane fragments: entry (s, L) = W[j = L&31][16s + 8(L>>5) + 0..7], split
   for (int e = (int)t; e < KS * 64; e += kWideNT) {
@@ -558,12 +564,12 @@ __global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __re
     float x[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) x[q] = (j < h && k0 + q < d) ? W[(size_t)j * dp + k0 + q] : 0.0f;
-    pbf16x8 hi, lo;
+    wh16x8 hi, lo;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const __bf16 hb = (__bf16)x[q];
+      const _Float16 hb = (_Float16)x[q];
       hi[q] = hb;
-      lo[q] = (__bf16)(x[q] - (float)hb);
+      lo[q] = (_Float16)(x[q] - (float)hb);
     }
     bfr[2 * e] = hi;
     bfr[2 * e + 1] = lo;
@@ -585,9 +591,9 @@ __global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __re
     const uint32_t row = g0 + r;
     const bool valid = row < n;
     const float* xr = X + (size_t)slots[valid ? row : g0] * dp;
-    pf32x16 acc;
+    pf32x16 acc, aab;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    for (int i = 0; i < 16; ++i) acc[i] = aab[i] = 0.0f;
     float ss = 0.0f;
     // 4 k-steps (64 columns) per round; the next round's loads are issued before this round's math
     float4 xa[4][2], xn4[4][2];
@@ -605,15 +611,19 @@ __global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __re
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (s0 + q < KS) {  // wave-uniform
-          pbf16x8 ah, al;
-          psplit8(xa[q][0], xa[q][1], ah, al);
+          wh16x8 ah, al, aa;
+          hsplit8(xa[q][0], xa[q][1], ah, al, aa);
           ss += xa[q][0].x * xa[q][0].x + xa[q][0].y * xa[q][0].y + xa[q][0].z * xa[q][0].z +
                 xa[q][0].w * xa[q][0].w + xa[q][1].x * xa[q][1].x + xa[q][1].y * xa[q][1].y +
                 xa[q][1].z * xa[q][1].z + xa[q][1].w * xa[q][1].w;
-          const pbf16x8 bh = bfr[2 * ((s0 + q) * 64 + lane)], bl = bfr[2 * ((s0 + q) * 64 + lane) + 1];
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+          const wh16x8 bh = bfr[2 * ((s0 + q) * 64 + lane)], bl = bfr[2 * ((s0 + q) * 64 + lane) + 1];
+          wh16x8 ba;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ba[e] = __builtin_fabsf16(bh[e]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+          aab = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa, ba, aab, 0, 0, 0);
         }
       }
 #pragma unroll
@@ -630,9 +640,10 @@ __global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __re
       const uint32_t ri = (i & 3) + 8u * (i >> 2) + 4u * hh;
       const float xni = __shfl(xn, (int)ri, 64);
       const float sv = acc[i];
+      const float bound = eps * (aab[i] * (1.0f + 0x1p-9f)) + abs_c * (wn + xni) + 0x1p-120f;
       const bool pos = col_ok && sv >= 0.0f;
-      const bool am = col_ok && (!(__builtin_fabsf(sv) > eps * wn * xni) || !(xni >= 0x1p-60f) ||
-                                 !(xni <= 0x1p60f));
+      // NaN / inf anywhere (S, T or the norms), or |S| within the bound: the exact chain decides
+      const bool am = col_ok && (!(__builtin_fabsf(sv) > bound) || !(xni <= 0x1p60f));
       const uint64_t bp = __ballot(pos), ba = __ballot(am);
       const uint32_t r0 = (i & 3) + 8u * (i >> 2);
       if (lane == r0) {
@@ -804,7 +815,8 @@ int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_
       KTime k1 = kt;
       k1.fold = -1;
       k_project_mfma_wide<<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h,
-                                                         key_or, project_eps(r.d), *pw, kt);
+                                                         key_or, wide_eps(r.d), wide_abs(r.d),
+                                                         *pw, kt);
       const uint32_t fcap = pw->fix_grid ? std::max(16u, pw->fix_grid) : 1024u;  // "fix_grid"
       k_project_fix<<<fcap, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
       return kPkWide;

@@ -1603,20 +1603,6 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
   }
 }
 
-template <int D, int RB, int NT, bool ROWS_LDS>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RB <= 192 ? 2 : 1))) void k_merge_big(const uint2* __restrict__ list, int cls,
-                                                  uint32_t* __restrict__ slots, Decider dc,
-                                                  Rows r, Counters* ctr, uint32_t* dlist,
-                                                  RunCounters* rc, KTime kt) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  kt_begin(kt, KC_BIG128 + cls);
-  const uint32_t count =
-      __hip_atomic_load(&rc->n_big[cls].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  big_runs<D, RB, NT, ROWS_LDS>(list, cls, count, blockIdx.x, gridDim.x, slots, dc, r, ctr, dlist,
-                                smem);
-  kt_end(kt, KC_BIG128 + cls);
-}
-
 constexpr uint32_t kHugeLdsRows = 8192;  // a huge run's slots and norms in LDS up to this length
 template <int D, int NT>
 __device__ __forceinline__ void huge_runs(const uint2* __restrict__ list, uint32_t count,
@@ -1624,6 +1610,30 @@ __device__ __forceinline__ void huge_runs(const uint2* __restrict__ list, uint32
                                           uint32_t* __restrict__ slots, const Decider& dc,
                                           const Rows& r, const MergeWork& w, Counters* ctr,
                                           unsigned char* smem);
+
+// One size class of 65..896-row runs (w.big[cls]).  w.huge_fold (385..896 class only): the
+// workgroups also walk the >896-row runs afterwards (huge_runs with NT lanes), so no k_merge_huge
+// is launched — the engine sets it after iterations without such runs, where a launch of its own
+// would have been empty.
+template <int D, int RB, int NT, bool ROWS_LDS>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RB <= 192 ? 2 : 1))) void k_merge_big(
+    MergeWork w, int cls, uint32_t* __restrict__ slots, Decider dc, Rows r, Counters* ctr) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  kt_begin(w.kt, KC_BIG128 + cls);
+  const uint32_t count =
+      __hip_atomic_load(&w.rc->n_big[cls].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  big_runs<D, RB, NT, ROWS_LDS>(w.big[cls], cls, count, blockIdx.x, gridDim.x, slots, dc, r, ctr,
+                                w.dlist, smem);
+  if constexpr (RB == kBigRows[kBigClasses - 1]) {
+    if (w.huge_fold) {
+      __syncthreads();  // (the LDS layouts overlap)
+      const uint32_t nh =
+          __hip_atomic_load(&w.rc->n_huge.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      huge_runs<D, NT>(w.huge, nh, blockIdx.x, gridDim.x, slots, dc, r, w, ctr, smem);
+    }
+  }
+  kt_end(w.kt, KC_BIG128 + cls);
+}
 
 // Small iterations: every merge class in ONE launch on the main stream (no fork/join across
 // streams, ≈35 us per iteration there): workgroups [0, nbig) take the 65..896-row runs (the
@@ -1908,6 +1918,7 @@ static size_t huge_lds(int d, int dp, int nt) {
 
 static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, const Rows& r,
                         Counters* ctr, uint32_t n, hipStream_t s) {
+  if (w.huge_fold) return;  // the 385..896-row kernel walks them (k_merge_big)
   const size_t lds = huge_lds(r.d, r.dp, kHugeNT);
   static const bool lds_ok = [] {
     bool ok = true;
@@ -2150,11 +2161,14 @@ struct BigWideLayout {
 };
 
 template <int RB, int NT, int KC>
-__global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__ list, int cls,
+__global__ __launch_bounds__(NT) void k_merge_big_wide(MergeWork w, int cls,
                                                        uint32_t* __restrict__ slots, Decider dc,
-                                                       Rows r, Counters* ctr, uint32_t* dlist,
-                                                       RunCounters* rc, KTime kt) {
+                                                       Rows r, Counters* ctr) {
   using L = BigWideLayout<RB, NT, KC>;
+  const uint2* __restrict__ list = w.big[cls];
+  uint32_t* const dlist = w.dlist;
+  RunCounters* const rc = w.rc;
+  const KTime kt = w.kt;
   kt_begin(kt, KC_BIG128 + cls);
   constexpr int W = L::W, NW = L::NW, STB = L::STB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2256,6 +2270,13 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(const uint2* __restrict__
                      reinterpret_cast<float*>(smem + L::tiles), wbuf, r, dc, slots, dlist, ctr);
     __syncthreads();
   }
+  if constexpr (RB == kBigRows[kBigClasses - 1]) {
+    if (w.huge_fold) {  // the >896-row runs too (see k_merge_big)
+      const uint32_t nh =
+          __hip_atomic_load(&w.rc->n_huge.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      huge_runs<0, NT>(w.huge, nh, blockIdx.x, gridDim.x, slots, dc, r, w, ctr, smem);
+    }
+  }
   kt_end(kt, KC_BIG128 + cls);
 }
 
@@ -2304,16 +2325,17 @@ template <int D, int RB, int NT, bool ROWS_LDS>
 static void launch_big(const MergeWork& w, int c, uint32_t* slots, const Decider& dc, const Rows& r,
                        Counters* ctr, uint32_t n, hipStream_t s) {
   using L = BigLayout<D, RB, ROWS_LDS>;
+  const bool fold = RB == kBigRows[kBigClasses - 1] && w.huge_fold;
+  const size_t lds = fold ? std::max(L::bytes, huge_lds(D, r.dp, NT)) : L::bytes;
   static const bool lds_ok = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_big<D, RB, NT, ROWS_LDS>),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)L::bytes) == hipSuccess;
+                               (int)std::max<size_t>(L::bytes, 96 * 1024)) == hipSuccess;
   }();
   (void)lds_ok;
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
   const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
-  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist,
-                                                           w.rc, w.kt);
+  k_merge_big<D, RB, NT, ROWS_LDS><<<g, NT, lds, s>>>(w, c, slots, dc, r, ctr);
 }
 
 // Fork the size-class kernels onto the auxiliary streams (after k_runs on s) and join them back
@@ -2404,16 +2426,17 @@ template <int RB, int NT, int KC>
 static void launch_big_wide(const MergeWork& w, int c, uint32_t* slots, const Decider& dc,
                             const Rows& r, Counters* ctr, uint32_t n, hipStream_t s) {
   using L = BigWideLayout<RB, NT, KC>;
+  const bool fold = RB == kBigRows[kBigClasses - 1] && w.huge_fold;
+  const size_t lds = fold ? std::max(L::bytes, huge_lds(r.d, r.dp, NT)) : L::bytes;
   static const bool lds_ok = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_merge_big_wide<RB, NT, KC>),
                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)L::bytes) == hipSuccess;
+                               (int)std::max<size_t>(L::bytes, 96 * 1024)) == hipSuccess;
   }();
   (void)lds_ok;
   const uint32_t lo = c == 0 ? 65u : (uint32_t)kBigRows[c - 1] + 1u;
   const uint32_t g = (uint32_t)std::min<uint64_t>(1024, n / lo + 1);
-  k_merge_big_wide<RB, NT, KC><<<g, NT, L::bytes, s>>>(w.big[c], c, slots, dc, r, ctr, w.dlist,
-                                                      w.rc, w.kt);
+  k_merge_big_wide<RB, NT, KC><<<g, NT, lds, s>>>(w, c, slots, dc, r, ctr);
 }
 
 static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc,

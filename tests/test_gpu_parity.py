@@ -255,6 +255,24 @@ def test_pcluster_run_lengths_vs_oracle(engine, oracle, b, d, groups, noise, thr
     assert_same_result(engine.result(), *oracle.pcluster(rows, thr))
 
 
+@pytest.mark.parametrize("b,d,groups,noise,thr", [
+    (3000, 32, 100, 0.05, 0.9), (2500, 64, 300, 0.08, 0.85), (1500, 16, 20, 0.03, 0.95),
+    (1200, 512, 40, 0.05, 0.9), (9000, 8, 900, 0.1, 0.8), (2000, 100, 2, 0.01, 0.9)])
+def test_pcluster_huge_runs_folded_vs_oracle(engine, oracle, b, d, groups, noise, thr):
+    """Runs over 896 rows walked by the 385..896-row kernel's 256-lane workgroups (option
+    "huge_fold", what the loop does after iterations without such runs) instead of k_merge_huge."""
+    rng = np.random.default_rng(b * 3 + d)
+    rows = clustered(rng, b, d, groups, noise)
+    engine.set_option("huge_fold", 1)
+    try:
+        engine.load_rows(rows)
+        engine.pcluster(thr)
+        got = engine.result()
+    finally:
+        engine.set_option("huge_fold", 0)
+    assert_same_result(got, *oracle.pcluster(rows, thr))
+
+
 def seq_sim(a, c):
     """The reference's sim for one pair, op by op in fp32 (distance.cc:27-38)."""
     f = np.float32
@@ -348,6 +366,24 @@ def test_cluster_random_vs_oracle(engine, oracle, n, d, groups, iters, bthr):
     assert np.array_equal(trace, o_trace)
     assert counter == o_counter
     assert_same_result(engine.result(), o_rows, o_off, o_ids)
+
+
+@pytest.mark.parametrize("n,d,groups,iters,bthr", [(50000, 16, 3, 3, 5000), (60000, 32, 20, 4, 1000000)])
+def test_cluster_huge_fold_vs_oracle(engine, oracle, n, d, groups, iters, bthr):
+    """The loop with every >896-row run walked inside the 385..896-row kernel (option huge_fold),
+    nested buckets included."""
+    rng = np.random.default_rng(n + d + 1)
+    rows = clustered(rng, n, d, groups, 0.05)
+    engine.set_option("huge_fold", 1)
+    try:
+        engine.load_rows(rows)
+        trace, counter, _ = engine.cluster(0.8, iters, bthr, 777, 3)
+        got = engine.result()
+    finally:
+        engine.set_option("huge_fold", 0)
+    o_rows, o_off, o_ids, o_trace, o_counter = oracle.cluster(rows, 0.8, iters, bthr, 777, 3)
+    assert np.array_equal(trace, o_trace) and counter == o_counter
+    assert_same_result(got, o_rows, o_off, o_ids)
 
 
 @pytest.mark.parametrize("window", [7, 40, 100])

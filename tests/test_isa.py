@@ -43,8 +43,8 @@ def test_projection_has_no_fused_multiply_add(kernels):
     for name, body in proj.items():
         bad = [ln.strip() for ln in body.splitlines() if FMA.match(ln)]
         assert not bad, (name, bad[:5])
-        if "mfma" in name:  # bf16x3 MFMA screen + the exact unfused chain for the close calls
-            assert "v_mfma_f32_32x32x16_bf16" in body, name
+        if "mfma" in name:  # fp16x3 MFMA screen + the exact unfused chain for the close calls
+            assert "v_mfma_f32_32x32x16_f16" in body, name
             assert "v_mul_f32" in body and "v_add_f32" in body, name
         elif "h16" in name:  # fp16-image screen (x~ . (w_hi + w_lo)) + the exact unfused chain
             assert "v_mfma_f32_32x32x16_f16" in body, name
