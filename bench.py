@@ -382,15 +382,19 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
                                                         "with the reference), packed v_pk_mul/v_pk_add"}
                 e["valu"]["frac"] = round(e["valu"]["achieved"] / VALU_PEAK_TFLOPS, 4)
             else:
-                # the certified screen: S = X W^T as bf16x3 (hi.hi + hi.lo + lo.hi), 3 bf16 MFMA
-                # products per f32 product, against the dense bf16 peak; the exact fix-up of the
-                # close calls is in the span too
-                fl = 3 * 2.0 * bits * d / k["launches"]
+                # the certified screen: S = X W^T as fp16x3 (hi.hi + hi.lo + lo.hi) plus the
+                # |x|.|w| bound product, 4 f16 MFMA products per f32 product, against the dense
+                # f16 peak; the exact fix-up of the close calls is in the span too
+                fl = 4 * 2.0 * bits * d / k["launches"]
                 e["mfma"] = {"achieved": round(fl / (avg * 1e-3) / 1e12, 2),
                              "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
-                             "note": "bf16x3 split on v_mfma_f32_32x32x16_bf16 (3 products per f32 "
-                                     "product); span includes k_project_fix"}
+                             "note": "fp16x3 split + |x|.|w| bound on v_mfma_f32_32x32x16_f16 (4 "
+                                     "products per f32 product); span includes k_project_fix"}
                 e["mfma"]["frac"] = round(e["mfma"]["achieved"] / BF16_DENSE_TFLOPS, 5)
+                fixed = sum(s.get("proj_fix_pairs", 0) for s in stats)
+                e["close_calls"] = {"pairs": fixed / steps, "frac_of_pairs": fixed / max(1, bits),
+                                    "note": "row-hyperplane pairs per step k_project_fix settled "
+                                            "with the exact f32 chains"}
         out.append(e)
     if not out:
         return {}

@@ -196,6 +196,14 @@ int klsh_hash_keys(klsh_ctx* ctx, const float* rows, uint64_t n, int d, const fl
  * keys in their original order. */
 int klsh_bucket_sort(klsh_ctx* ctx, const uint32_t* keys, uint64_t n, int bits,
                      uint32_t* sorted_keys, uint32_t* perm);
+/* The buckets of n sorted keys as the merge step takes them (the runs of equal keys; the
+ * reference's lsh_table entries, function/cluster.cc:205-300): every run of 2 or more keys in start
+ * order with its length and its list (0..5: 2, 3-4, 5-8, 9-16, 17-32, 33-64 rows; 6..9: 65-128,
+ * 129-192, 193-384, 385-896; 10: longer; 11: longer than bucket_thr >= 0, i.e. nestedCluster).
+ * *n_runs: in, the capacity of the outputs; out, the run count (KLSH_E_RANGE if it exceeds the
+ * capacity).  A test hook. */
+int klsh_bucket_runs(klsh_ctx* ctx, const uint32_t* sorted_keys, uint64_t n, int bucket_thr,
+                     uint64_t* n_runs, uint32_t* starts, uint32_t* lengths, int32_t* lists);
 /* p_cluster (reference function/cluster.cc:56-87) over the loaded rows taken as ONE bucket in
  * load order, at threshold thr.  Afterwards klsh_count/klsh_result give the survivors. */
 int klsh_pcluster(klsh_ctx* ctx, float thr);

@@ -36,7 +36,7 @@ EXPORTED = (
     "klsh_comm_info", "klsh_set_option", "klsh_get_option", "klsh_wrs", "klsh_ttest2", "klsh_fastq_open",
     "klsh_fastq_next", "klsh_fastq_close", "klsh_kset_create", "klsh_kset_destroy",
     "klsh_check_reads", "klsh_extract_fastq", "klsh_build_khtable", "klsh_cuckoo_order",
-    "klsh_kmc_info",
+    "klsh_kmc_info", "klsh_bucket_runs",
 )
 
 
@@ -170,6 +170,8 @@ def load_library() -> ctypes.CDLL:
                                           ctypes.c_int, _P]),
         "klsh_bucket_sort": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, _P, _P]),
         "klsh_pcluster": (ctypes.c_int, [_P, ctypes.c_float]),
+        "klsh_bucket_runs": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, _u64p, _P, _P,
+                                            _P]),
         "klsh_hyperplanes": (ctypes.c_int, [ctypes.c_uint32, _u64p, ctypes.c_int,
                                             ctypes.c_int, _P]),
         "klsh_fp_selftest": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _P, _P]),
@@ -489,6 +491,20 @@ class Engine:
         _check(self._lib.klsh_bucket_sort(self._ctx, _ptr(keys), keys.size, bits, _ptr(out),
                                           _ptr(perm)), "klsh_bucket_sort")
         return out, perm
+
+    def bucket_runs(self, sorted_keys: np.ndarray, bucket_thr: int):
+        """The merge step's runs of equal sorted keys: (starts, lengths, lists), start order."""
+        k = np.ascontiguousarray(sorted_keys, dtype=np.uint32)
+        cap = k.size // 2 + 1
+        st = np.zeros(cap, np.uint32)
+        ln = np.zeros(cap, np.uint32)
+        li = np.zeros(cap, np.int32)
+        nr = ctypes.c_uint64(cap)
+        _check(self._lib.klsh_bucket_runs(self._ctx, _ptr(k), k.size, int(bucket_thr),
+                                          ctypes.byref(nr), _ptr(st), _ptr(ln), _ptr(li)),
+               "klsh_bucket_runs")
+        m = nr.value
+        return st[:m], ln[:m], li[:m]
 
     def fp_selftest(self, a: np.ndarray, b: np.ndarray):
         a = np.ascontiguousarray(a, np.float32)

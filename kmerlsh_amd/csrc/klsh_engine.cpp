@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -1943,6 +1944,79 @@ int klsh_bucket_sort(klsh_ctx* ctx, const uint32_t* keys, uint64_t n, int bits,
   (void)hipStreamSynchronize(s);
   release();
   return rc;
+}
+
+// The run finding of merge_main alone on caller keys (a test hook): every run of 2+ equal keys
+// of n sorted keys with its list, in start order.
+int klsh_bucket_runs(klsh_ctx* ctx, const uint32_t* sorted_keys, uint64_t n, int bucket_thr,
+                     uint64_t* n_runs, uint32_t* starts, uint32_t* lengths, int32_t* lists) {
+  if (!ctx || !n_runs || (n && !sorted_keys)) return fail(KLSH_E_ARG, "null argument");
+  if (n >= 0xFFFFFFF0ull) return fail(KLSH_E_RANGE, "keys >= 2^32");
+  const uint64_t cap = *n_runs;
+  *n_runs = 0;
+  if (n == 0) return 0;
+  KLSH_HIP(hipSetDevice(ctx->device));
+  using klsh::kBigClasses;
+  using klsh::kGroupClasses;
+  klsh::MergeWork w{};
+  uint32_t* dk = nullptr;
+  klsh::RunCounters* rc = nullptr;
+  auto release = [&] {
+    dfree(dk); dfree(rc); dfree(w.run_ws); dfree(w.huge); dfree(w.over);
+    for (auto& c : w.cls) dfree(c);
+    for (auto& c : w.big) dfree(c);
+  };
+  int e = 0;
+  if ((e = dalloc(&dk, n)) || (e = dalloc(&rc, 1)) || (e = dalloc(&w.run_ws, klsh::run_ws_words(n))) ||
+      (e = dalloc(&w.huge, n / 897 + 64)) || (e = dalloc(&w.over, n / 2 + 64))) {
+    release();
+    return e;
+  }
+  for (int c = 0; c < kGroupClasses && !e; ++c) e = dalloc(&w.cls[c], klsh::group_class_capacity(c, n));
+  for (int c = 0; c < kBigClasses && !e; ++c)
+    e = dalloc(&w.big[c], n / ((c ? klsh::kBigRows[c - 1] : 64) + 1) + 64);
+  if (e) {
+    release();
+    return e;
+  }
+  w.rc = rc;
+  w.kt = klsh::kNoTime;
+  hipStream_t s = ctx->stream;
+  klsh::RunCounters hc{};
+  int rc_ = 0;
+  if (hipMemsetAsync(rc, 0, sizeof(*rc), s) != hipSuccess ||
+      hipMemcpyAsync(dk, sorted_keys, 4 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+    rc_ = fail(KLSH_E_HIP, "upload");
+  } else {
+    klsh::launch_runs(dk, 0, (uint32_t)n, bucket_thr, w, s);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(&hc, rc, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc_ = fail(KLSH_E_HIP, "run finding");
+  }
+  std::vector<std::array<uint32_t, 3>> runs;  // (start, length, list)
+  auto take = [&](const uint2* list, uint32_t count, int l) -> int {
+    std::vector<uint2> h(count);
+    if (count && hipMemcpy(h.data(), list, sizeof(uint2) * count, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(KLSH_E_HIP, "list copy");
+    for (const uint2& x : h) runs.push_back({x.x, x.y, (uint32_t)l});
+    return 0;
+  };
+  for (int c = 0; c < kGroupClasses && !rc_; ++c) rc_ = take(w.cls[c], hc.n_cls[c].v, c);
+  for (int c = 0; c < kBigClasses && !rc_; ++c) rc_ = take(w.big[c], hc.n_big[c].v, kGroupClasses + c);
+  if (!rc_) rc_ = take(w.huge, hc.n_huge.v, klsh::kRunListCount - 2);
+  if (!rc_) rc_ = take(w.over, hc.n_over.v, klsh::kRunListCount - 1);
+  release();
+  if (rc_) return rc_;
+  std::sort(runs.begin(), runs.end());
+  *n_runs = runs.size();
+  if (runs.size() > cap) return fail(KLSH_E_RANGE, "more runs than the output holds (see *n_runs)");
+  for (size_t i = 0; i < runs.size(); ++i) {
+    if (starts) starts[i] = runs[i][0];
+    if (lengths) lengths[i] = runs[i][1];
+    if (lists) lists[i] = (int32_t)runs[i][2];
+  }
+  return 0;
 }
 
 int klsh_pcluster(klsh_ctx* ctx, float thr) {

@@ -53,9 +53,9 @@ struct RunCounters {
   CountLine n_big_rows[kBigClasses], n_huge_rows;  // rows in the big / huge runs (kernel rooflines)
 };
 
-// Run-finding workspace (u32 words) for `slots` positions: 19 counts + a tail end + a 4096-bit
-// head bitmap per 4096-position tile.
-inline uint64_t run_ws_words(uint64_t slots) { return (slots / 4096 + 2) * (19 + 1 + 128) + 64; }
+// Run-finding workspace (u32 words) for `slots` positions: 19 counts + a tail end + the first /
+// last heads + a 4096-bit head bitmap per 4096-position tile.
+inline uint64_t run_ws_words(uint64_t slots) { return (slots / 4096 + 2) * (19 + 1 + 2 + 128) + 64; }
 
 // Device-side per-iteration counters (zeroed by the host before each iteration).
 struct Counters {
@@ -252,6 +252,13 @@ void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
                   float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s,
                   const uint32_t* n_dev = nullptr);
+
+// Bucket runs of positions [lo, lo + n) of sorted keys (n_dev: the count read on the device, as
+// launch_merge): every run of 2+ equal keys into its list of w (size classes, big classes, huge,
+// oversize), the counts into w.rc.  (launch_merge's first step; klsh_bucket_runs for tests.)
+constexpr int kRunListCount = kGroupClasses + kBigClasses + 2;
+void launch_runs(const uint32_t* key, uint32_t lo, uint32_t n, int bucket_thr, const MergeWork& w,
+                 hipStream_t s, const uint32_t* n_dev = nullptr);
 
 // Counters handed to the host through mapped pinned memory (no copy launch, no stream sync): the
 // compaction's last workgroup writes *ctr (total filled in) to `host`, zeroes *ctr for the next

@@ -611,14 +611,8 @@ __device__ __forceinline__ uint32_t* run_counter(RunCounters* rc, int l) {
                                            : &rc->n_huge_rows.v;
 }
 
-// The run starting at tile-local position q (a head of bitmap hb): its length and list (-1: one row).
-__device__ __forceinline__ int run_list(const uint64_t* hb, uint32_t T0, uint32_t tail_end,
-                                        uint32_t q, int bucket_thr, uint32_t& b) {
-  uint32_t wi = q >> 6;
-  uint64_t m = hb[wi] & ~((2ull << (q & 63u)) - 1ull);  // heads after q in its word
-  while (!m && ++wi < kRunTile / 64) m = hb[wi];
-  const uint32_t next = m ? T0 + wi * 64u + (uint32_t)__builtin_ctzll(m) : tail_end;
-  b = next - (T0 + q);
+// The list of a run of b rows (-1: one row).
+__device__ __forceinline__ int run_class(uint32_t b, int bucket_thr) {
   if (bucket_thr >= 0 && b > (uint32_t)bucket_thr) return kRunLists - 1;  // cluster.cc:286
   if (b > 64u) {
     if (b > (uint32_t)kBigRows[kBigClasses - 1]) return kRunLists - 2;
@@ -629,17 +623,60 @@ __device__ __forceinline__ int run_list(const uint64_t* hb, uint32_t T0, uint32_
   return b >= 2 ? size_class(b) : -1;
 }
 
+// What run counter `l` (kRunRows of them) receives for a run of b rows in list lr.
+__device__ __forceinline__ uint32_t run_contrib(int l, int lr, uint32_t b) {
+  if (l < kRunLists) return l == lr ? 1u : 0u;
+  if (l == kRunLists) return 0u;  // heads: counted where the head is found
+  if (l == kRunLists + 1) return (lr >= 0 && lr < kGroupClasses) ? b : 0u;
+  if (l < kRunLists + 2 + kBigClasses) return lr == kGroupClasses + (l - kRunLists - 2) ? b : 0u;
+  return lr == kRunLists - 2 ? b : 0u;
+}
+
+// Exclusive suffix minimum over the 256 threads of a workgroup: min of v over threads > t (~0u if
+// none).  Every thread must call it.
+__device__ __forceinline__ uint32_t block_excl_suffix_min_256(uint32_t v) {
+  __shared__ uint32_t sm[256];
+  const uint32_t t = threadIdx.x;
+  sm[t] = v;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive suffix min, Hillis-Steele
+    const uint32_t u = t + o < 256 ? sm[t + o] : ~0u;
+    __syncthreads();
+    sm[t] = min(sm[t], u);
+    __syncthreads();
+  }
+  const uint32_t r = t + 1 < 256 ? sm[t + 1] : ~0u;
+  __syncthreads();
+  return r;
+}
+
+// The run starting at tile-local position q (a head of bitmap hb): its length and list (-1: one row).
+__device__ __forceinline__ int run_list(const uint64_t* hb, uint32_t T0, uint32_t tail_end,
+                                        uint32_t q, int bucket_thr, uint32_t& b) {
+  uint32_t wi = q >> 6;
+  uint64_t m = hb[wi] & ~((2ull << (q & 63u)) - 1ull);  // heads after q in its word
+  while (!m && ++wi < kRunTile / 64) m = hb[wi];
+  const uint32_t next = m ? T0 + wi * 64u + (uint32_t)__builtin_ctzll(m) : tail_end;
+  b = next - (T0 + q);
+  return run_class(b, bucket_thr);
+}
+
+// Per tile: the head bitmap, the first head (global position, ~0u = none) and the last head
+// (tile-local, ~0u = none), and per-list counts of every run that starts in the tile EXCEPT its
+// last one: that run's end is the first head of a later tile (tail_end), found by a suffix minimum
+// over the tiles' first heads in the scan / write kernel — so no tile walks forward past its end
+// (linear in n at any run length).
 __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__ key, uint32_t lo,
                                                     uint32_t n, int bucket_thr, uint32_t ntiles,
                                                     uint64_t* __restrict__ hbits,
-                                                    uint32_t* __restrict__ tail_ends,
+                                                    uint2* __restrict__ heads_fl,
                                                     uint32_t* __restrict__ counts, KTime kt,
                                                     const uint32_t* __restrict__ n_dev) {
   kt_begin(kt, KC_RUNS);
   if (n_dev) n = *n_dev;  // tiles past it find no heads and count nothing
   __shared__ uint64_t hb[kRunTile / 64];
   __shared__ uint32_t lcnt[kRunRows];
-  __shared__ uint32_t s_tail_end;
+  __shared__ uint32_t s_last;
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t T0 = blockIdx.x * kRunTile;
   if (t < (uint32_t)kRunRows) lcnt[t] = 0u;
@@ -660,24 +697,23 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
       hbits[(size_t)blockIdx.x * (kRunTile / 64) + k * 4 + wv] = m;
     }
   }
-  if (wv == 0) {  // the end of the tile's last run: the first head at or after T0 + kRunTile
-    uint32_t j = T0 + kRunTile, end = n;
-    while (j < n) {
-      const uint32_t q = j + lane;
-      const uint64_t m = __ballot(q < n && kp[q] != kp[q - 1]);
-      if (m) {
-        end = j + (uint32_t)__builtin_ctzll(m);
-        break;
-      }
-      j += 64u;
+  __syncthreads();
+  if (wv == 0) {  // the tile's first and last heads (bitmap word `lane`)
+    const uint64_t m = hb[lane];
+    const uint64_t nz = __ballot(m != 0ull);
+    uint32_t first = ~0u, last = ~0u;
+    if (nz) {
+      const uint32_t wf = (uint32_t)__builtin_ctzll(nz), wl = 63u - (uint32_t)__builtin_clzll(nz);
+      first = T0 + wf * 64u + (uint32_t)__builtin_ctzll(hb[wf]);
+      last = wl * 64u + 63u - (uint32_t)__builtin_clzll(hb[wl]);
     }
     if (lane == 0) {
-      s_tail_end = min(end, n);
-      tail_ends[blockIdx.x] = min(end, n);
+      s_last = last;
+      heads_fl[blockIdx.x] = make_uint2(first, last);
     }
   }
   __syncthreads();
-  const uint32_t tail_end = s_tail_end;
+  const uint32_t lastq = s_last;
   const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   uint32_t heads = 0, small_rows = 0;
   uint32_t lrows[kBigClasses + 1] = {};  // rows per big class, then huge
@@ -686,13 +722,15 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
     const uint32_t q = (uint32_t)k * 256u + t;
     int l = -1;
     if ((hb[q >> 6] >> (q & 63u)) & 1ull) {
-      uint32_t b;
-      l = run_list(hb, T0, tail_end, q, bucket_thr, b);
       ++heads;
-      if (l >= 0 && l < kGroupClasses) small_rows += b;
+      if (q != lastq) {  // (the last run's list: the scan / write kernel)
+        uint32_t b;
+        l = run_list(hb, T0, 0u, q, bucket_thr, b);
+        if (l >= 0 && l < kGroupClasses) small_rows += b;
 #pragma unroll
-      for (int c = 0; c <= kBigClasses; ++c)
-        if (l == kGroupClasses + c) lrows[c] += b;
+        for (int c = 0; c <= kBigClasses; ++c)
+          if (l == kGroupClasses + c) lrows[c] += b;
+      }
     }
     // lanes with the same list: one LDS add by the lowest of them
     const uint32_t id = (uint32_t)(l + 1);  // 0 = no entry
@@ -720,15 +758,39 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
   if (t < (uint32_t)kRunRows) counts[(size_t)t * ntiles + blockIdx.x] = lcnt[t];
 }
 
-// Workgroup l: counts[l][0..ntiles) -> exclusive prefix over the tiles; the total -> list l's counter.
+// The last run of tile j (tile-local head `last`, ~0u = none) ends at tail_end: its length.
+__device__ __forceinline__ uint32_t last_run_len(uint32_t j, uint32_t last, uint32_t tail_end) {
+  return last == ~0u ? 0u : tail_end - (j * kRunTile + last);
+}
+
+// Workgroup l: the tiles' last runs (their ends from a suffix minimum over the first heads; list
+// 0's workgroup writes the tail ends) into counts[l], then counts[l][0..ntiles) -> exclusive prefix
+// over the tiles; the total -> list l's counter.
 __global__ __launch_bounds__(256) void k_runs_scan(uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                   uint32_t n, int bucket_thr,
+                                                   const uint2* __restrict__ heads_fl,
+                                                   uint32_t* __restrict__ tail_ends,
                                                    RunCounters* rc) {
-  uint32_t* row = counts + (size_t)blockIdx.x * ntiles;
+  const int l = (int)blockIdx.x;
+  uint32_t* row = counts + (size_t)l * ntiles;
   const uint32_t t = threadIdx.x;
   const uint32_t per = (ntiles + 255u) / 256u;
   const uint32_t a = min(ntiles, t * per), e = min(ntiles, a + per);
+  uint32_t fmin = ~0u;  // first head of this thread's tiles
+  for (uint32_t i = a; i < e; ++i) fmin = min(fmin, heads_fl[i].x);
+  uint32_t after = block_excl_suffix_min_256(fmin);  // first head after this thread's tiles
   uint32_t acc = 0;
-  for (uint32_t i = a; i < e; ++i) acc += row[i];
+  for (uint32_t i = e; i-- > a;) {  // reverse: `after` is the first head after tile i
+    const uint2 hf = heads_fl[i];
+    const uint32_t te = min(after, n);
+    if (l == 0) tail_ends[i] = te;
+    const uint32_t b = last_run_len(i, hf.y, te);
+    uint32_t v = row[i];
+    if (b) v += run_contrib(l, run_class(b, bucket_thr), b);
+    row[i] = v;
+    acc += v;
+    after = min(after, hf.x);
+  }
   uint32_t total;
   uint32_t run = block_excl_scan_256(acc, &total);
   for (uint32_t i = a; i < e; ++i) {
@@ -736,29 +798,41 @@ __global__ __launch_bounds__(256) void k_runs_scan(uint32_t* __restrict__ counts
     row[i] = run;
     run += v;
   }
-  if (t == 0) *run_counter(rc, (int)blockIdx.x) = total;
+  if (t == 0) *run_counter(rc, l) = total;
 }
 
 // SCAN (ntiles <= 256, every iteration below 2^20 positions): `counts` are the raw per-tile counts
-// and each workgroup sums its own list bases (the tiles before it; thread t holds tile t) — and
-// workgroup 0 the list totals — so k_runs_scan is not launched: one dependent launch less.
+// and each workgroup sums its own list bases (the tiles before it; thread t holds tile t, and adds
+// tile t's last run once the suffix minimum of the first heads gives its end) — and workgroup 0
+// the list totals — so k_runs_scan is not launched: one dependent launch less.
 template <bool SCAN>
-__global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, int bucket_thr, uint32_t ntiles,
+__global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, uint32_t n, int bucket_thr,
+                                                    uint32_t ntiles,
                                                     const uint64_t* __restrict__ hbits,
+                                                    const uint2* __restrict__ heads_fl,
                                                     const uint32_t* __restrict__ tail_ends,
                                                     const uint32_t* __restrict__ counts,
-                                                    MergeWork w) {
+                                                    MergeWork w, const uint32_t* __restrict__ n_dev) {
   __shared__ uint64_t hb[kRunTile / 64];
   __shared__ uint32_t lbase[kRunLists], lfill[kRunLists];
+  __shared__ uint32_t s_tail_end;
   const uint32_t t = threadIdx.x;
   const uint32_t T0 = blockIdx.x * kRunTile;
   if (t < kRunTile / 64) hb[t] = hbits[(size_t)blockIdx.x * (kRunTile / 64) + t];
   if constexpr (SCAN) {
+    if (n_dev) n = *n_dev;
     __shared__ uint32_t red[2][4][kRunRows];
     const uint32_t lane = t & 63u, wv = t >> 6;
     uint32_t cv[kRunRows];  // every load in flight before the reductions
 #pragma unroll
     for (int l = 0; l < kRunRows; ++l) cv[l] = t < ntiles ? counts[(size_t)l * ntiles + t] : 0u;
+    const uint2 hf = t < ntiles ? heads_fl[t] : make_uint2(~0u, ~0u);
+    const uint32_t te = min(block_excl_suffix_min_256(hf.x), n);  // the end of tile t's last run
+    if (t == blockIdx.x) s_tail_end = te;
+    const uint32_t lb = t < ntiles ? last_run_len(t, hf.y, te) : 0u;
+    const int lr = lb ? run_class(lb, bucket_thr) : -1;
+#pragma unroll
+    for (int l = 0; l < kRunRows; ++l) cv[l] += lb ? run_contrib(l, lr, lb) : 0u;
 #pragma unroll
     for (int l = 0; l < kRunRows; ++l) {
       const uint32_t v = cv[l];
@@ -785,9 +859,10 @@ __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, int bucket_thr,
       lbase[t] = counts[(size_t)t * ntiles + blockIdx.x];
       lfill[t] = 0u;
     }
+    if (t == 0) s_tail_end = tail_ends[blockIdx.x];
   }
   __syncthreads();
-  const uint32_t tail_end = tail_ends[blockIdx.x];
+  const uint32_t tail_end = s_tail_end;
 #pragma unroll 4
   for (int k = 0; k < 16; ++k) {
     const uint32_t q = (uint32_t)k * 256u + t;
@@ -2470,6 +2545,28 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
   group(k_merge_group_wide<2>, 0, 32);
 }
 
+void launch_runs(const uint32_t* key, uint32_t lo, uint32_t n, int bucket_thr, const MergeWork& w,
+                 hipStream_t s, const uint32_t* n_dev) {
+  const uint32_t ntiles = (n + kRunTile - 1) / kRunTile;
+  // run_ws: counts [kRunRows][ntiles], tail ends [ntiles], then 8-byte aligned: first / last
+  // heads (uint2) [ntiles], head bitmaps [ntiles][64]
+  uint32_t* counts = w.run_ws;
+  uint32_t* tail_ends = counts + (size_t)kRunRows * ntiles;
+  uint2* heads_fl = reinterpret_cast<uint2*>(counts + (((kRunRows + 1u) * ntiles + 1u) & ~1u));
+  uint64_t* hbits = reinterpret_cast<uint64_t*>(heads_fl + ntiles);
+  k_runs_count<<<ntiles, 256, 0, s>>>(key, lo, n, bucket_thr, ntiles, hbits, heads_fl, counts,
+                                      w.kt, n_dev);
+  const bool fused = ntiles <= 256u;  // the write kernel scans the counts itself
+  if (fused) {
+    k_runs_write<true><<<ntiles, 256, 0, s>>>(lo, n, bucket_thr, ntiles, hbits, heads_fl,
+                                              tail_ends, counts, w, n_dev);
+  } else {
+    k_runs_scan<<<kRunRows, 256, 0, s>>>(counts, ntiles, n, bucket_thr, heads_fl, tail_ends, w.rc);
+    k_runs_write<false><<<ntiles, 256, 0, s>>>(lo, n, bucket_thr, ntiles, hbits, heads_fl,
+                                               tail_ends, counts, w, nullptr);
+  }
+}
+
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
                   float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s,
                   const uint32_t* n_dev) {
@@ -2477,17 +2574,7 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   const uint32_t n = hi - lo;
   if (n_dev && (lo != 0 || n >= kTailMergeMax)) return;  // (the caller checks)
   const Decider dc = make_decider(thr);
-  const uint32_t ntiles = (n + kRunTile - 1) / kRunTile;
-  uint32_t* counts = w.run_ws;
-  uint32_t* tail_ends = counts + (size_t)kRunRows * ntiles;
-  // 8-byte aligned: counts + tail ends take (kRunRows + 1) * ntiles words, rounded up to even
-  uint64_t* hbits = reinterpret_cast<uint64_t*>(counts + (((kRunRows + 1u) * ntiles + 1u) & ~1u));
-  k_runs_count<<<ntiles, 256, 0, s>>>(key, lo, n, bucket_thr, ntiles, hbits, tail_ends, counts,
-                                      w.kt, n_dev);
-  const bool fused = ntiles <= 256u;  // the write kernel scans the counts itself
-  if (!fused) k_runs_scan<<<kRunRows, 256, 0, s>>>(counts, ntiles, w.rc);
-  if (fused) k_runs_write<true><<<ntiles, 256, 0, s>>>(lo, bucket_thr, ntiles, hbits, tail_ends, counts, w);
-  else k_runs_write<false><<<ntiles, 256, 0, s>>>(lo, bucket_thr, ntiles, hbits, tail_ends, counts, w);
+  launch_runs(key, lo, n, bucket_thr, w, s, n_dev);
   switch (r.d) {
     case 8: launch_groups<8>(r, slots, dc, w, ctr, n, s); break;
     case 16: launch_groups<16>(r, slots, dc, w, ctr, n, s); break;

@@ -219,6 +219,62 @@ def test_cluster_variants_agree(engine, oracle, d):
     assert len(set(seen)) == 1, seen
 
 
+def runs_reference(keys, bucket_thr):
+    """Runs of equal keys (the buckets merge_hashtable fills, cluster.cc:15-30) of 2+ rows with the
+    merge step's list: size class by length, > bucket_thr = nestedCluster (cluster.cc:286)."""
+    n = keys.size
+    heads = np.flatnonzero(np.concatenate([[True], keys[1:] != keys[:-1]])) if n else np.zeros(0, int)
+    lens = np.diff(np.concatenate([heads, [n]]))
+    keep = lens >= 2
+    heads, lens = heads[keep], lens[keep]
+    lists = np.empty(lens.size, np.int32)
+    for i, b in enumerate(lens):
+        if bucket_thr >= 0 and b > bucket_thr:
+            lists[i] = 11
+        elif b > 896:
+            lists[i] = 10
+        elif b > 64:
+            lists[i] = 6 + int(np.searchsorted([128, 192, 384, 896], b))
+        else:
+            lists[i] = int(np.searchsorted([2, 4, 8, 16, 32, 64], b))
+    return heads.astype(np.uint32), lens.astype(np.uint32), lists
+
+
+@pytest.mark.parametrize("case", ["random", "giant", "giant_over", "tile_edges", "all_equal",
+                                  "singletons", "long_mixed", "fused_giant"])
+def test_bucket_runs_vs_reference(engine, case):
+    """Run finding at any run length (a 4.2M-key run spans ~1000 tiles: linear, no per-tile
+    forward walk), oversize runs (nestedCluster's list), runs ending exactly on tile edges; both
+    the fused (<= 256 tiles) and the scanned path."""
+    rng = np.random.default_rng(len(case))
+    thr = -1
+    if case == "random":
+        keys = np.sort(rng.integers(0, 200_000, 1_500_000)).astype(np.uint32)
+    elif case in ("giant", "giant_over"):
+        keys = np.sort(np.concatenate([rng.integers(0, 1 << 20, 800_000),
+                                       np.full(4_200_000, 777_777)])).astype(np.uint32)
+        thr = 1_000_000 if case == "giant_over" else -1
+    elif case == "tile_edges":
+        lens = rng.choice([1, 2, 63, 64, 65, 896, 897, 4095, 4096, 4097, 8192], 3000)
+        keys = np.repeat(np.arange(lens.size, dtype=np.uint32), lens)
+        thr = 4096
+    elif case == "all_equal":
+        keys = np.zeros(3_000_000, np.uint32)
+    elif case == "singletons":
+        keys = np.arange(2_000_000, dtype=np.uint32)
+    elif case == "long_mixed":
+        lens = rng.integers(1, 20000, 400)
+        keys = np.repeat(np.arange(lens.size, dtype=np.uint32) * 3, lens)
+        thr = 9000
+    else:  # fused: <= 256 tiles with a run across all of them
+        keys = np.concatenate([np.zeros(5, np.uint32), np.full(900_000, 9, np.uint32),
+                               np.arange(10, 100_010, dtype=np.uint32)])
+    got = engine.bucket_runs(keys, thr)
+    want = runs_reference(keys, thr)
+    for g, w_ in zip(got, want):
+        assert np.array_equal(g, w_), case
+
+
 # ------------------------------------------------------------------------------ p_cluster ---
 @pytest.mark.parametrize("name", ["pcluster_small", "pcluster_large", "pcluster_generic",
                                   "pcluster_d8"])
