@@ -279,7 +279,9 @@ def pmc_traffic(config, kernel):
 #   project   rows x (4d row + 4 slot + 4 key)
 #   sort      sum over iterations of N_t x passes_t x 20 (hist: key; scatter: key + slot in and out)
 #   runs      rows x 4 (sorted keys) + runs x 8 (list entries)
-#   small     rows x (4d + 4) (row + slot) + merges x (4d + 20) (new row, norm, count, head, link)
+#   small     rows x (4d + 4) (row + slot) + merges x (4d + 20) (new row, norm, count, head, link);
+#             after the screen, its rows are those of the runs the screen passed
+#   screen    rows x (2d + 4) (fp16 row + slot) + runs x 8 (list entries)
 #   big*/huge rows x (4d + 20) (row, slot, count, head, tail, the slot written back)
 #   tail      rows x (4d + 8) (all merge classes of a small iteration in one launch)
 #   compact   rows x 12 (slots read twice, survivors written)
@@ -289,7 +291,7 @@ KERNEL_NAMES = {
     "big128": "k_merge_big<{d},128,128,true>", "big192": "k_merge_big<{d},192,256,true>",
     "big384": "k_merge_big<{d},384,256,true>", "big896": "k_merge_big<{d},896,256,false>",
     "huge": "k_merge_huge<{d}>", "tail": "k_merge_tail<{d}>",
-    "compact": "k_compact_count/apply (span)",
+    "compact": "k_compact_count/apply (span)", "screen": "k_small_screen<{d}>",
 }
 WIDE_NAMES = {
     "project": "k_project_mfma_wide + k_project_fix (span)",
@@ -323,6 +325,7 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
             continue
         rows, runs = k["rows"], k["runs"]
         b = {"project": rows * (row_bytes + 8), "sort": sort_bytes, "runs": rows * 4 + runs * 8,
+             "screen": rows * (2 * d + 4) + runs * 8,
              "small": rows * (4 * d + 4) + merges_small * (4 * d + 20),
              "tail": rows * (4 * d + 8), "compact": rows * 12}.get(c, rows * (4 * d + 20))
         avg = k["ms"] / k["launches"]
@@ -423,6 +426,8 @@ def main():
                     help="profiling only: run the sharded loop on one GPU (in-process group of 1)")
     ap.add_argument("--iterations", type=int, default=0,
                     help="profiling only: override the config's -I (the metric is then not C2's)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine option (klsh_set_option), e.g. small_screen=1; repeatable")
     args = ap.parse_args()
 
     world, rank, local = dist_setup()
@@ -437,6 +442,9 @@ def main():
     eng = _native.Engine(local)
     if args.phases:
         eng.set_option("phase_timing", 1)
+    for opt in args.option:
+        name, _, val = opt.partition("=")
+        eng.set_option(name, int(val))
     sharded = world > 1 and args.mode == "sharded"
     if sharded:
         import torch.distributed as dist
@@ -524,6 +532,8 @@ def main():
         "nested_calls_per_step": agg["nested_calls"] / args.steps,
         "parity": parity,
     }
+    if args.option:
+        line["options"] = args.option
     print(json.dumps(line), flush=True)
     if parity.get("checked") and not parity["ok"]:
         sys.exit(1)  # a fast wrong answer is not a result

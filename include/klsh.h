@@ -39,7 +39,7 @@ extern "C" {
 
 /* ABI version of this header.  2: every statistics struct starts with `struct_size`, which the
  * caller sets to sizeof(the struct) (the library refuses a mismatch instead of writing past a
- * smaller struct); klsh_stats.kern has KLSH_KCLASSES = 11 classes; klsh_get_option. */
+ * smaller struct); klsh_stats.kern has KLSH_KCLASSES = 12 classes; klsh_get_option. */
 #define KLSH_ABI_VERSION 2
 
 typedef struct klsh_ctx klsh_ctx;
@@ -59,7 +59,8 @@ typedef struct klsh_ctx klsh_ctx;
 #define KLSH_K_HUGE 8     /* longer runs (k_merge_huge) */
 #define KLSH_K_TAIL 9     /* iterations below 2^20 positions: every merge class in one k_merge_tail */
 #define KLSH_K_COMPACT 10 /* survivor compaction (span) */
-#define KLSH_KCLASSES 11
+#define KLSH_K_SCREEN 11  /* fp16 screen of the runs of 2..64 rows (SMALL then merges the ones left) */
+#define KLSH_KCLASSES 12
 typedef struct klsh_kstat {
   double ms;
   uint64_t launches;
@@ -156,6 +157,8 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *   "phase_timing"     0/1: per-phase HIP events (adds latency; default 0)
  *   "kernel_timing"    0/1: the per-class statistics of klsh_stats.kern (default 1)
  *   "tail_batch"       0/1: queue the small late iterations 32 at a time (default 1)
+ *   "tail_local"       0/1: their bucket sort as a top-10-bit pass + per-bucket LDS sorts that
+ *                      also list the runs (default 1; 0 = the LSD passes + run kernels)
  *   "huge_fold"        1 (tests): runs over 896 rows always walked inside the 385..896-row
  *                      kernel (default 0: only after several iterations without such runs)
  *   "projection"       0 = the certified matrix-core screens where they exist (default: the fp16
@@ -168,7 +171,12 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *                      iterations' worth)
  *   "comm_timeout_s"   a collective still incomplete after this many seconds aborts (default 600)
  *   launch sizes, 0 = the measured default: "h16_grid", "wide_grid", "fix_grid" (projection),
- *   "small_grid", "tail_big_groups", "tail_small_groups", "wide_group_grid" (merge);
+ *   "small_grid", "tail_big_groups", "tail_small_groups", "wide_group_grid",
+ *   "small_screen_grid" (merge);
+ *   "small_screen"     1 = runs of 2..64 rows are screened on the fp16 row image first and only
+ *                      the ones the screen cannot rule out are merged on the f32 rows
+ *   "tail_merge_rows"  iterations below this many rows merge every class in one launch (default
+ *                      2^20; tests lower it to reach the per-class launches at small sizes)
  *   "h16_segcap" (tests) caps the fp16 projection's per-workgroup fix-up segment. */
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
 /* Any option above, plus read-only diagnostics: "fp16_image" (1 = the loaded rows have the fp16

@@ -44,8 +44,8 @@ EXPORTED = (
 ABI_VERSION = 2
 # klsh_stats.kern indices (include/klsh.h KLSH_K_*)
 KERNEL_CLASSES = ("project", "sort", "runs", "small", "big128", "big192", "big384", "big896",
-                  "huge", "tail", "compact")
-KCLASSES = 11
+                  "huge", "tail", "compact", "screen")
+KCLASSES = 12
 
 
 class KlshKstat(ctypes.Structure):

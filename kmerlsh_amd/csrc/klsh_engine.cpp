@@ -185,8 +185,10 @@ struct klsh_ctx {
   bool shadow_wanted(int d_) const {
     return pw.variant != klsh::kProjPacked && klsh::shadow_width_ok(d_);
   }
-  // Queued tail batches (run_batched; option "tail_batch", default on)
+  // Queued tail batches (run_batched; option "tail_batch", default on), their bucket sort as a
+  // top-bits pass + the LDS bucket sort that lists the runs (option "tail_local", default on)
   bool tail_batch = true;
+  bool tail_local = true;
   // klsh_hash_keys diagnostics (klsh_get_option): the projection kernel of the last call and
   // the (row, hyperplane) pairs its screen left to the exact chains
   int last_hash_kernel = klsh::kPkNone;
@@ -274,6 +276,7 @@ struct klsh_ctx {
     pw.cap = 0;
     for (auto& c : mw.big) dfree(c);
     for (auto& c : mw.cls) dfree(c);
+    for (auto& c : mw.act) dfree(c);
     dfree(kstamp);
     dfree(lb.status);
     dfree(xh_alloc);
@@ -357,7 +360,8 @@ struct klsh_ctx {
       }
     }
     for (int c = 0; c < klsh::kGroupClasses; ++c) {
-      if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s)))) {
+      if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s))) ||
+          (e = dalloc(&mw.act[c], klsh::group_class_capacity(c, s)))) {
         release_state();
         return e;
       }
@@ -555,8 +559,14 @@ static void count_class_rows(klsh_stats* st, const Counters& c, uint64_t n, bool
     st->kern[KC_TAIL].runs += small_runs + big_runs;
     return;
   }
-  st->kern[KC_SMALL].rows += c.n_small_rows;
-  st->kern[KC_SMALL].runs += small_runs;
+  if (c.screened) {  // the screen saw every small run, the merge only the ones it passed
+    st->kern[KC_SCREEN].rows += c.n_small_rows;
+    st->kern[KC_SCREEN].runs += small_runs;
+    st->kern[KC_SMALL].rows += c.n_act_rows;
+  } else {
+    st->kern[KC_SMALL].rows += c.n_small_rows;
+    st->kern[KC_SMALL].runs += small_runs;
+  }
   for (int b = 0; b < kBigClasses; ++b) {
     st->kern[KC_BIG128 + b].rows += c.n_big_rows[b];
     st->kern[KC_BIG128 + b].runs += c.n_big[b];
@@ -874,7 +884,7 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
   // the small-run merge is a launch of its own at >= 2^20 positions (register widths): its HIP
   // events are the headline's cross-check
-  const bool time_small = kt.blk && st && sync && n >= (1u << 20) &&
+  const bool time_small = kt.blk && st && sync && n >= klsh::tail_merge_max(ctx->mw) &&
                           klsh::project_device_n_ok(ctx->d);
   ctx->mw.small_ev[0] = time_small ? ctx->sev[0] : nullptr;
   ctx->mw.small_ev[1] = time_small ? ctx->sev[1] : nullptr;
@@ -901,14 +911,14 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
     if (int e = ctx->sync_counters()) return e;
   }
   if (kt.blk && st) {  // this iteration's rows per kernel class
-    const bool tail = n < (1u << 20) && klsh::project_device_n_ok(ctx->d);
+    const bool tail = n < klsh::tail_merge_max(ctx->mw) && klsh::project_device_n_ok(ctx->d);
     count_class_rows(st, *ctx->h_ctr, n, tail);
   }
   if (time_small) {  // the compaction (published) runs after the merge streams' join
     KLSH_HIP(hipEventSynchronize(ctx->sev[1]));
     st->small_ms += elapsed(ctx->sev[0], ctx->sev[1]);
     st->small_launches += 1;
-    st->small_rows += ctx->h_ctr->n_small_rows;
+    st->small_rows += ctx->h_ctr->screened ? ctx->h_ctr->n_act_rows : ctx->h_ctr->n_small_rows;
     st->small_iter_merges += n - ctx->h_ctr->total;
   }
   if (timed && zc) KLSH_HIP(hipEventSynchronize(ctx->ev[4]));
@@ -1013,7 +1023,8 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
 // ring slot and the host reads a chunk's slots when its last sequence number is in — the trace,
 // the RNG counter and the statistics come out exactly as the per-iteration loop's.
 static bool batch_eligible(const klsh_ctx* ctx, uint64_t n, int bucket_thr, int iters_left) {
-  if (!ctx->tail_batch || n < 2 || n >= (1u << 20) || iters_left < 2) return false;
+  if (!ctx->tail_batch || n < 2 || n >= klsh::tail_merge_max(ctx->mw) || iters_left < 2)
+    return false;
   if (bucket_thr >= 0 && n > (uint64_t)bucket_thr) return false;
   if (!ctx->zero_copy || !ctx->ring_dev || !ctx->lb.status || ctx->phase_timing) return false;
   if (!klsh::project_device_n_ok(ctx->d) || ctx->mw.dlist) return false;
@@ -1068,11 +1079,22 @@ static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, 
                                       n_dev, s, kt, woff_dev, &ctx->pw);
       queued = false;
       uint32_t *fk = nullptr, *fv = nullptr;
-      klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n_max, hb,
-                       ctx->hist, &fk, &fv, s, kt, n_dev);
-      ctx->mw.kt = kt;
+      const bool local = ctx->tail_local && klsh::tail_local_ok((uint32_t)n_max, hb);
+      if (local) {  // top-bits partition, then the buckets sorted in LDS with their runs listed
+        const uint32_t* dtot = klsh::radix_sort_top(ctx->keys, ctx->order, ctx->keys2, ctx->alt,
+                                                    (uint32_t)n_max, hb, ctx->hist, s, kt, n_dev);
+        ctx->mw.kt = kt;
+        klsh::launch_tail_local(ctx->keys2, ctx->alt, ctx->keys, ctx->order, dtot, hb,
+                                bucket_size_threshold, ctx->mw, s);
+        fk = ctx->keys;
+        fv = ctx->order;
+      } else {
+        klsh::radix_sort(ctx->keys, ctx->order, ctx->keys2, ctx->alt, (uint32_t)n_max, hb,
+                         ctx->hist, &fk, &fv, s, kt, n_dev);
+        ctx->mw.kt = kt;
+      }
       klsh::launch_merge(ctx->rows, fk, fv, 0, (uint32_t)n_max, thr, bucket_size_threshold,
-                         ctx->mw, ctx->ctr, s, n_dev);
+                         ctx->mw, ctx->ctr, s, n_dev, local);
       ctx->mw.kt = klsh::kNoTime;
       uint32_t* out = (fv == ctx->order) ? ctx->alt : ctx->order;
       klsh::Publish pub{ctx->ring_dev + slot, ctx->pub_seq_dev, ++ctx->pub_seq, n_dev, woff_dev};
@@ -1699,6 +1721,7 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   if (n == "kernel_timing") return flag(&ctx->kernel_timing);
   if (n == "tail_batch") return flag(&ctx->tail_batch);
   if (n == "huge_fold") return flag(&ctx->huge_fold_always);
+  if (n == "tail_local") return flag(&ctx->tail_local);
   if (n == "hyperplane_window") {
     if (value < 0) return fail(KLSH_E_ARG, "hyperplane_window must be >= 0");
     ctx->hyperplane_window = (uint64_t)value;
@@ -1730,6 +1753,17 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   if (n == "tail_big_groups") return grid(&ctx->mw.tail_nbig);
   if (n == "tail_small_groups") return grid(&ctx->mw.tail_nsmall);
   if (n == "wide_group_grid") return grid(&ctx->mw.wide_group_grid);
+  if (n == "small_screen_grid") return grid(&ctx->mw.screen_grid);
+  if (n == "tail_merge_rows") {
+    if (value < 0 || value > (1 << 20)) return fail(KLSH_E_ARG, "tail_merge_rows must be in [0, 2^20]");
+    ctx->mw.tail_max = (uint32_t)value;
+    return 0;
+  }
+  if (n == "small_screen") {
+    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "small_screen must be 0 or 1");
+    ctx->mw.small_screen = (uint32_t)value;
+    return 0;
+  }
   return fail(KLSH_E_ARG, "unknown option " + n);
 }
 
@@ -1741,6 +1775,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "kernel_timing") *value = ctx->kernel_timing;
   else if (n == "tail_batch") *value = ctx->tail_batch;
   else if (n == "huge_fold") *value = ctx->huge_fold_always;
+  else if (n == "tail_local") *value = ctx->tail_local;
   else if (n == "hyperplane_window") *value = (int64_t)ctx->hyperplane_window;
   else if (n == "stop_after") *value = ctx->stop_after;
   else if (n == "projection") *value = ctx->pw.variant;
@@ -1753,6 +1788,9 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "tail_big_groups") *value = ctx->mw.tail_nbig;
   else if (n == "tail_small_groups") *value = ctx->mw.tail_nsmall;
   else if (n == "wide_group_grid") *value = ctx->mw.wide_group_grid;
+  else if (n == "small_screen_grid") *value = ctx->mw.screen_grid;
+  else if (n == "tail_merge_rows") *value = klsh::tail_merge_max(ctx->mw);
+  else if (n == "small_screen") *value = ctx->mw.small_screen;
   else if (n == "fp16_image") *value = ctx->rows.xh != nullptr;
   else if (n == "last_hash_kernel") *value = ctx->last_hash_kernel;
   else if (n == "last_hash_close_pairs") *value = (int64_t)ctx->last_hash_close;

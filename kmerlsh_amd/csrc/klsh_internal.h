@@ -51,6 +51,9 @@ struct alignas(128) CountLine {
 struct RunCounters {
   CountLine n_seg, n_cls[kGroupClasses], n_big[kBigClasses], n_huge, n_over, n_small_rows;
   CountLine n_big_rows[kBigClasses], n_huge_rows;  // rows in the big / huge runs (kernel rooflines)
+  // the small-run screen (k_small_screen): runs of each class it could not rule out, their rows,
+  // and a flag that it ran this iteration
+  CountLine n_act[kGroupClasses], n_act_rows, screened;
 };
 
 // Run-finding workspace (u32 words) for `slots` positions: 19 counts + a tail end + the first /
@@ -70,6 +73,8 @@ struct Counters {
   uint32_t n_small_rows;           // rows in the runs of 2..64 rows (the small-run merge's rows)
   uint32_t n_big_rows[kBigClasses];  // rows in the runs of each big class
   uint32_t n_huge_rows;            // rows in the runs of k_merge_huge
+  uint32_t n_act_rows;             // rows in the small runs the screen passed to k_merge_small
+  uint32_t screened;               // 1: the small-run screen ran this iteration
 };
 
 // Per-kernel-class timing (bench.py's roofline) from in-kernel stamps: every workgroup of a timed
@@ -84,7 +89,7 @@ struct Counters {
 // order) and clears it; the engine folds the last set at the end of a call.
 enum KClass : int {
   KC_PROJECT = 0, KC_SORT, KC_RUNS, KC_SMALL, KC_BIG128, KC_BIG192, KC_BIG384, KC_BIG896, KC_HUGE,
-  KC_TAIL, KC_COMPACT, KC_COUNT
+  KC_TAIL, KC_COMPACT, KC_SCREEN, KC_COUNT
 };
 constexpr int kStampSlots = 16;
 struct alignas(128) StampLine {
@@ -113,6 +118,10 @@ constexpr KTime kNoTime{nullptr, 0, -1};
 // Merge workspace (device), sized for `cap` positions.
 struct MergeWork {
   uint2* cls[kGroupClasses];       // (start, length) of runs per size class
+  // the runs of each class the fp16 screen could not rule out (k_small_screen), and whether the
+  // small-run merge reads these instead of cls (set per launch)
+  uint2* act[kGroupClasses];
+  uint32_t screened;
   uint2* big[kBigClasses];         // (start, length) of runs for k_merge_big, per class
   uint2* huge;                     // (start, length) of runs for k_merge_huge
   uint2* over;                     // (start, length) of oversize runs
@@ -144,6 +153,11 @@ struct MergeWork {
   uint32_t tail_nbig;        // "tail_big_groups": k_merge_tail's big-run workgroups
   uint32_t tail_nsmall;      // "tail_small_groups": k_merge_tail's small-run workgroups
   uint32_t wide_group_grid;  // "wide_group_grid": the wide-row group merges, per class
+  uint32_t screen_grid;      // "small_screen_grid": the small-run screen's persistent launch
+  uint32_t small_screen;     // "small_screen": 1 = screen the small runs on the fp16 image first
+  // "tail_merge_rows": below this many positions every merge class runs in ONE launch
+  // (k_merge_tail); 0 = the default 2^20 (tests lower it to reach the per-class launches)
+  uint32_t tail_max;
   hipStream_t aux[3];
   KTime kt;                // per-class stamps of this iteration's merge launches
   hipEvent_t small_ev[2];  // HIP events around the small-run launch (nullptr: not recorded)
@@ -151,6 +165,7 @@ struct MergeWork {
   hipEvent_t join[3];
 };
 constexpr int kMergeStreams = 3;
+inline uint32_t tail_merge_max(const MergeWork& w) { return w.tail_max ? w.tail_max : (1u << 20); }
 
 // Row state, structure-of-arrays, one entry per slot (a slot is a row of the loaded matrix;
 // a merge writes the consensus into the candidate's slot, cluster.cc:70-74).
@@ -249,9 +264,25 @@ void radix_sort(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t
 // bucket_thr (>= 0) are queued to w.over (start, length) and left untouched.
 // n_dev (may be null; lo == 0 and hi < 2^20 only): the position count is read on the device
 // (<= hi, which sizes the grids).
+// runs_ready: the run lists of [lo, hi) are already built (launch_tail_local).
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
                   float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s,
-                  const uint32_t* n_dev = nullptr);
+                  const uint32_t* n_dev = nullptr, bool runs_ready = false);
+
+// Small iterations (< 2^20 positions, keys of 11..20 bits): the stable bucket sort in two steps
+// that also builds the run lists.  radix_sort_top: the stable partition of (k0, v0) by the top 10
+// of `bits` key bits into (k1, v1); returns the top buckets' sizes (1024 words).
+// launch_tail_local: every top bucket of (k1, v1) sorted stably by its low bits-10 bits into
+// (k0, v0), and its runs of 2+ equal keys listed into w (as launch_runs would).
+const uint32_t* radix_sort_top(const uint32_t* k0, const uint32_t* v0, uint32_t* k1, uint32_t* v1,
+                               uint32_t n, int bits, uint32_t* ws, hipStream_t s, KTime kt,
+                               const uint32_t* n_dev);
+void launch_tail_local(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
+                       const uint32_t* dtot, int bits, int bucket_thr, const MergeWork& w,
+                       hipStream_t s);
+inline bool tail_local_ok(uint32_t n_max, int bits) {
+  return n_max <= (1u << 20) && bits >= 11 && bits <= 20;
+}
 
 // Bucket runs of positions [lo, lo + n) of sorted keys (n_dev: the count read on the device, as
 // launch_merge): every run of 2+ equal keys into its list of w (size classes, big classes, huge,

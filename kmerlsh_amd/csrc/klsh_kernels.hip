@@ -903,6 +903,12 @@ __device__ __forceinline__ void collect_run_counts(Counters* ctr, RunCounters* r
   }
   ctr->n_huge_rows = rc->n_huge_rows.v;
   rc->n_huge_rows.v = 0u;
+#pragma unroll
+  for (int c = 0; c < kGroupClasses; ++c) rc->n_act[c].v = 0u;
+  ctr->n_act_rows = rc->n_act_rows.v;
+  rc->n_act_rows.v = 0u;
+  ctr->screened = rc->screened.v;
+  rc->screened.v = 0u;
 }
 
 // Publish the iteration's counters to the host (see Publish), `total` filled in.

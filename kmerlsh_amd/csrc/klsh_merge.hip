@@ -498,8 +498,9 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
                                            float* lds, uint32_t wave, uint32_t nwaves) {
   constexpr int NC = kGroupClasses;
   uint32_t n[NC], nb[NC], start[NC + 1];
-  const CountLine* counts = w.rc->n_cls;
-  const uint2* const* lists = w.cls;
+  // after the fp16 screen: only the runs it could not rule out (the others merge nothing)
+  const CountLine* counts = w.screened ? w.rc->n_act : w.rc->n_cls;
+  const uint2* const* lists = w.screened ? w.act : w.cls;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
     n[c] = __hip_atomic_load(&counts[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -573,6 +574,261 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
   }
 }
 
+
+// ------------------------------------------------- the fp16 screen of the small runs -----
+// Every run of 2..64 rows is first tested on the fp16 row image (Rows::xh, half the bytes of the
+// f32 rows): a run can merge only if some pair (a, b) passes cosine >= s* (cluster.cc:66-69), and
+//   |x~a.x~b / (|x~a| |x~b|) - fl(dot_ref / fl(sqrtf(nrm_a) sqrtf(nrm_b)))| <= m
+// with m = m0 + a2 (1/|x~a| + 1/|x~b|): the fp16 rounding of both rows (2^-11 each, relative, plus
+// 2^-25 absolute per element for subnormals), the screen's f32 sums, the reference's own sequential
+// sums and the quotient's roundings, 1.5x headroom (screen_margins).  A run none of whose pairs
+// reaches s* - m cannot merge: it is left as it is — the walk's result for it is "no change" — and
+// only the others go on to k_merge_small (lists MergeWork::act), which decides them exactly on the
+// f32 rows.  A row whose image has no usable norm (zero, tiny, fp16 overflow, NaN) keeps its run.
+//
+// The screen is a gather of 64 fp16 rows per batch followed by little arithmetic (the Gram blocks
+// on the matrix cores), so what bounds it is the bytes in flight: each wave keeps the rows of the
+// next kAhead batches loading in registers while it screens one (and the slots and list entries
+// of the batches after those), so a wave has up to kAhead * 8 KB of row loads outstanding instead
+// of waiting for one batch at a time.  One wave per workgroup; the batches of every class (64/G
+// runs of G lanes, lane g = position g) in one persistent space, most expensive class first;
+// passed runs collect in LDS per class and go out 32+ at a time (one atomic per flush).
+typedef _Float16 sh16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 sh16x2 __attribute__((ext_vector_type(2)));
+typedef float pf16acc __attribute__((ext_vector_type(16)));
+typedef float pf4acc __attribute__((ext_vector_type(4)));
+#ifndef KLSH_SCREEN_AHEAD
+#define KLSH_SCREEN_AHEAD 2
+#endif
+#ifndef KLSH_SCREEN_WPE
+#define KLSH_SCREEN_WPE 2
+#endif
+constexpr int kScreenAhead = KLSH_SCREEN_AHEAD;  // batches whose rows are in flight while one is screened
+
+template <int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_WPE))) void k_small_screen(MergeWork w, const uint32_t* __restrict__ slots,
+                                                     Rows r, float s_star, float m0, float a2,
+                                                     KTime kt) {
+  constexpr int NC = kGroupClasses, STH = D + 8;  // LDS row stride in halves (16-B pad)
+  constexpr int NR = kScreenAhead + 1;            // row buffers: the screened batch + the ones ahead
+  constexpr uint32_t kBuf = 256;                  // passed runs kept in LDS before a flush
+  __shared__ __attribute__((aligned(16))) _Float16 lrow[64 * STH];
+  __shared__ float linv[64];
+  __shared__ uint32_t lflag[64];  // per run of the batch: some pair not ruled out
+  __shared__ uint2 buf[kBuf];     // passed runs (start, length | class << 16)
+  __shared__ uint32_t fcnt[NC], fbase[NC];
+  kt_begin(kt, KC_SCREEN);
+  const uint32_t lane = __lane_id();
+  if (blockIdx.x == 0 && lane == 0) w.rc->screened.v = 1u;
+  uint32_t n[NC], nb[NC], start[NC + 1];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    // (scalar: every batch index and class below is wave-uniform, so list pointers stay in SGPRs
+    // and no vector load of a pointer makes the wave wait for its outstanding row loads)
+    n[c] = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&w.rc->n_cls[c].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t per = 32u >> c;  // runs per batch: 64 / G, G = 2 << c
+    nb[c] = (n[c] + per - 1u) / per;
+  }
+  {
+    uint32_t a = 0;
+#pragma unroll
+    for (int c = NC - 1; c >= 0; --c) {
+      start[c] = a;
+      a += nb[c];
+    }
+    start[NC] = a;
+  }
+  const uint32_t total = start[NC], stride = gridDim.x;
+  uint32_t nbuf = 0, brows = 0;  // (wave-uniform)
+  // this wave's passed runs to the global lists: per class, one add and the entries
+  auto flush = [&]() {
+    if (lane < (uint32_t)NC) fcnt[lane] = 0u;
+    wave_lds_fence();
+    for (uint32_t i = lane; i < nbuf; i += 64) atomicAdd(&fcnt[buf[i].y >> 16], 1u);
+    wave_lds_fence();
+    if (lane < (uint32_t)NC) {
+      const uint32_t c = fcnt[lane];
+      fbase[lane] = c ? atomicAdd(&w.rc->n_act[lane].v, c) : 0u;
+      fcnt[lane] = 0u;
+    }
+    if (lane == 0 && brows) atomicAdd(&w.rc->n_act_rows.v, brows);
+    wave_lds_fence();
+    for (uint32_t i = lane; i < nbuf; i += 64) {
+      const uint2 e = buf[i];
+      const uint32_t c = e.y >> 16;
+      const uint32_t at = fbase[c] + atomicAdd(&fcnt[c], 1u);
+      w.act[c][at] = make_uint2(e.x, e.y & 0xFFFFu);
+    }
+    wave_lds_fence();
+    nbuf = brows = 0u;
+  };
+  const uint64_t below = lanes_below(lane);
+  auto class_of = [&](uint32_t t) -> int {  // (wave-uniform: t is)
+    int c = 0;
+#pragma unroll
+    for (int q = NC - 1; q >= 0; --q)
+      if (t >= start[q] && t < start[q] + nb[q]) c = q;
+    return __builtin_amdgcn_readfirstlane(c);
+  };
+  auto list_of = [&](int c) -> const uint2* {
+    return c == 0 ? w.cls[0] : c == 1 ? w.cls[1] : c == 2 ? w.cls[2] : c == 3 ? w.cls[3]
+         : c == 4 ? w.cls[4] : w.cls[5];
+  };
+  // Every load below is unconditional (a lane with nothing to load reads a valid dummy address),
+  // so the loads of the batches ahead are never waited for early: the compiler counts them.
+  // the lane's run entry in batch t ((0, 0) past the end)
+  auto entry_of = [&](uint32_t t) -> uint2 {
+    const int c = class_of(t);
+    const uint32_t G = 2u << c, NG = 64u / G;
+    const uint32_t k = (t - start[c]) * NG + lane / G;
+    const bool ok = t < total && k < n[c];
+    const uint2 e = list_of(c)[ok ? k : 0u];  // (every list holds >= 64 entries)
+    return ok ? e : make_uint2(0u, 0u);
+  };
+  auto slot_of = [&](uint32_t t, const uint2& e) -> uint32_t {
+    const uint32_t g = lane & ((2u << class_of(t)) - 1u);
+    return slots[g < e.y ? e.x + g : e.x];
+  };
+  auto load_rows = [&](uint32_t slot, sh16x8 (&x)[D / 8]) {
+    const uint16_t* src = r.xh + (size_t)slot * r.dp;
+#pragma unroll
+    for (int q = 0; q < D / 8; ++q) x[q] = *reinterpret_cast<const sh16x8*>(src + 8 * q);
+  };
+  // one batch: rows x (arrived), entry e
+  auto screen = [&](uint32_t t, const uint2& e, const sh16x8 (&x)[D / 8]) {
+    const int c = class_of(t);
+    const uint32_t G = 2u << c;
+    const uint32_t g = lane & (G - 1);
+    const uint32_t b = e.y;
+    const bool valid = g < b;
+    float ss = 0.0f;
+#pragma unroll
+    for (int q = 0; q < D / 8; ++q) {
+      *reinterpret_cast<sh16x8*>(lrow + lane * STH + 8 * q) = valid ? x[q] : sh16x8{};
+#pragma unroll
+      for (int hi2 = 0; hi2 < 8; hi2 += 2) {
+        const sh16x2 v = {x[q][hi2], x[q][hi2 + 1]};
+        ss = __builtin_amdgcn_fdot2(v, v, ss, false);
+      }
+    }
+    // a row without a usable norm (zero, tiny, fp16 overflow, NaN) cannot be screened: its run
+    // goes to the exact merge
+    const bool bad = valid && !(ss >= 0x1p-100f && ss <= 0x1p100f);
+    const uint32_t lg = (uint32_t)__builtin_ctz(G);  // log2 G
+    linv[lane] = valid && !bad ? 1.0f / __builtin_sqrtf(ss) : 0.0f;
+    lflag[lane] = 0u;
+    wave_lds_fence();
+    if (bad) lflag[lane >> lg] = 1u;
+    const uint64_t vmask = __ballot(valid && !bad);  // rows the Gram test reads
+    // The Gram blocks of the batch's runs on the matrix cores (x~ . x~ exact products, f32 sums):
+    // 32 x 32 tiles for runs of 17..64 rows (the upper-triangular tiles of each run), 16 x 16
+    // diagonal tiles for shorter runs (4 per batch, runs never cross a 16-row block).  A pair
+    // (R < C) of one run that the screen cannot rule out flags the run in LDS.
+    auto test = [&](uint32_t R, uint32_t C, float sv) {
+      if (R < C && (R >> lg) == (C >> lg) && ((vmask >> R) & (vmask >> C) & 1ull)) {
+        const float ir = linv[R], ic = linv[C];
+        const float qv = sv * ir * ic;
+        const float m = m0 + a2 * (ir + ic);
+        if (!(qv < s_star - m)) lflag[R >> lg] = 1u;  // NaN / inf: not ruled out
+      }
+    };
+    if constexpr (D < 32) {  // (not launched: screen_ok needs d >= 32) rule nothing out
+      lflag[lane] = 1u;
+    } else if (G >= 32u) {
+      const uint32_t r32 = lane & 31u, k8 = 8u * (lane >> 5);
+#pragma unroll 1
+      for (int tt = 0; tt < 3; ++tt) {
+        const uint32_t tr = tt == 2 ? 1u : 0u, tc = tt == 0 ? 0u : 1u;
+        if (G == 32u && tt == 1) continue;  // two runs: their diagonal tiles only
+        pf16acc acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+          const sh16x8 fa = *reinterpret_cast<const sh16x8*>(lrow + (tr * 32u + r32) * STH + 16 * ks + k8);
+          const sh16x8 fb = *reinterpret_cast<const sh16x8*>(lrow + (tc * 32u + r32) * STH + 16 * ks + k8);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          test(tr * 32u + (uint32_t)(q & 3) + 8u * (uint32_t)(q >> 2) + 4u * (lane >> 5),
+               tc * 32u + r32, acc[q]);
+      }
+    } else {
+      const uint32_t r16 = lane & 15u, k8 = 8u * (lane >> 4);
+#pragma unroll 1
+      for (int tb = 0; tb < 4; ++tb) {
+        pf4acc acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) {
+          const sh16x8 f = *reinterpret_cast<const sh16x8*>(lrow + (16u * tb + r16) * STH + 32 * ks + k8);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(f, f, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          test(16u * tb + 4u * (lane >> 4) + (uint32_t)q, 16u * tb + r16, acc[q]);
+      }
+    }
+    wave_lds_fence();
+    const bool grp = lflag[lane >> lg] != 0u;
+    const bool leader = g == 0u && b >= 2u && grp;
+    const uint64_t lead = __ballot(leader);
+    if (lead) {
+      if (nbuf + 64u > kBuf) flush();  // (rare: the buffer holds a wave's passed runs)
+      if (leader)
+        buf[nbuf + (uint32_t)__popcll(lead & below)] = make_uint2(e.x, b | ((uint32_t)c << 16));
+      uint32_t rsum = leader ? b : 0u;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) rsum += (uint32_t)__shfl_xor((int)rsum, o, 64);
+      nbuf += (uint32_t)__popcll(lead);
+      brows += rsum;
+    }
+    wave_lds_fence();  // the rows of this batch are read before the next batch overwrites them
+  };
+  // The pipeline (batches t0, t0 + stride, ...): batch j is screened while the rows of j+1 ..
+  // j+kAhead, the slot of j+kAhead+1 and the entries of j+kAhead+1, j+kAhead+2 are in flight.
+  // Row buffers rotate through NR register arrays (the loop is unrolled NR times so every index
+  // is static).
+  sh16x8 xb[NR][D / 8];
+  uint2 eb[NR];  // entries of the batches whose rows are (to be) in xb (same index)
+  const uint32_t t0 = blockIdx.x;
+  {
+    uint2 e0[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) e0[k] = entry_of(t0 + (uint32_t)k * stride);
+#pragma unroll
+    for (int k = 0; k < NR - 1; ++k) {
+      eb[k] = e0[k];
+      load_rows(slot_of(t0 + (uint32_t)k * stride, e0[k]), xb[k]);
+    }
+    eb[NR - 1] = e0[NR - 1];
+  }
+  uint32_t s_next = slot_of(t0 + (uint32_t)(NR - 1) * stride, eb[NR - 1]);
+  uint2 e_next = entry_of(t0 + (uint32_t)NR * stride);
+  // Issue order matters: the slot and entry loads go out BEFORE the row loads, so that waiting
+  // for them next step (vmcnt counts in issue order) leaves the rows in flight.
+  auto step = [&](uint32_t t, int cur) {  // cur: the buffer of batch t
+    const int nxt = (cur + NR - 1) % NR;  // the buffer of batch t + kAhead * stride
+    const uint32_t ta = t + (uint32_t)NR * stride;
+    const uint32_t s_rows = s_next;       // slot of batch t + kAhead (arrived a step ago)
+    s_next = slot_of(ta, e_next);
+    const uint2 e_after = entry_of(ta + stride);
+    load_rows(s_rows, xb[nxt]);
+    const uint2 e_cur = eb[cur];
+    eb[cur] = e_next;  // batch t + NR * stride's rows go to this buffer next time round
+    e_next = e_after;
+    screen(t, e_cur, xb[cur]);
+  };
+  // (whole rounds of NR steps: a batch past the end screens nothing, and a branch-free body
+  // keeps the compiler's count of the loads in flight exact across the loop)
+  for (uint32_t t = t0; t < total; t += (uint32_t)NR * stride) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) step(__builtin_amdgcn_readfirstlane(t + (uint32_t)k * stride), k);
+  }
+  if (nbuf) flush();
+  kt_end(kt, KC_SCREEN);
+}
 
 template <int D>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_merge_small(
@@ -877,6 +1133,173 @@ __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, uint32_t n, int
       else if (l == kRunLists - 2) w.huge[at] = e;
       else w.over[at] = e;
     }
+  }
+  kt_end(w.kt, KC_RUNS);
+}
+
+// ------------------------------------------- small iterations: local bucket sort + runs -----
+// Below 2^20 positions the stable bucket order (merge_hashtable, cluster.cc:15-30) is built in two
+// steps: a stable partition by the top 10 key bits (radix_sort_top: one hist / dscan / scatter
+// pass), then this kernel — workgroup d takes top bucket d, a contiguous range of the partition in
+// canonical order, and sorts it stably by the remaining `lb` low bits (a counting sort in LDS:
+// digit counts, their exclusive scan, then ranks among equal digits in position order from wave
+// ballots, 4096 keys per round).  Equal keys of one top bucket have equal low bits, so the runs
+// of the iteration are exactly the low digits with a count >= 2: their (start, length) entries
+// come straight from the digit counts, classified as k_runs_write does (run_class), with one
+// list-counter add per list per bucket — the whole run finding of these iterations without the
+// tile kernels (k_runs_count / k_runs_write) or the second radix pass (3 launches).
+__global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__ kin,
+                                                    const uint32_t* __restrict__ vin,
+                                                    uint32_t* __restrict__ kout,
+                                                    uint32_t* __restrict__ vout,
+                                                    const uint32_t* __restrict__ dtot, int lb,
+                                                    int bucket_thr, MergeWork w) {
+  constexpr uint32_t kChunk = 4096, kItems = 16;
+  __shared__ uint32_t cnt[1024];      // low-digit counts, then their exclusive starts
+  __shared__ uint32_t run_[1024];     // running count of each digit over the rounds
+  __shared__ uint32_t wc[4][1024];    // per-wave digit counts of a round, then wave prefixes
+  __shared__ uint32_t lcnt[kRunRows];  // this bucket's list counts, rows, heads
+  __shared__ uint32_t lbase[kRunLists];
+  __shared__ uint32_t red[4];
+  kt_begin(w.kt, KC_RUNS);
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t d = blockIdx.x;
+  const uint32_t RAD = 1u << lb, MASK = RAD - 1u;
+  // the bucket: [base, base + m) of the partition
+  uint32_t part = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t i = t * 4u + (uint32_t)q;
+    part += i < d ? dtot[i] : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  if (lane == 0) red[wv] = part;
+  for (uint32_t i = t; i < 1024u; i += 256) {
+    cnt[i] = 0u;
+    run_[i] = 0u;
+    wc[0][i] = wc[1][i] = wc[2][i] = wc[3][i] = 0u;
+  }
+  if (t < (uint32_t)kRunRows) lcnt[t] = 0u;
+  __syncthreads();
+  const uint32_t base = red[0] + red[1] + red[2] + red[3];
+  const uint32_t m = dtot[d];
+  if (m == 0u) {
+    kt_end(w.kt, KC_RUNS);
+    return;
+  }
+  // 1. low-digit counts
+  for (uint32_t i = t; i < m; i += 256) atomicAdd(&cnt[kin[base + i] & MASK], 1u);
+  __syncthreads();
+  // 2. the runs (digits with a count >= 2) per list, and the digit starts
+  uint32_t c4[4], acc = 0, heads = 0, small_rows = 0;
+  uint32_t lrows[kBigClasses + 1] = {};
+  int l4[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t dg = t * 4u + (uint32_t)q;
+    c4[q] = dg < RAD ? cnt[dg] : 0u;
+    acc += c4[q];
+    heads += c4[q] ? 1u : 0u;
+    l4[q] = c4[q] >= 2u ? run_class(c4[q], bucket_thr) : -1;
+    if (l4[q] >= 0) {
+      atomicAdd(&lcnt[l4[q]], 1u);
+      if (l4[q] < kGroupClasses) small_rows += c4[q];
+#pragma unroll
+      for (int c = 0; c <= kBigClasses; ++c)
+        if (l4[q] == kGroupClasses + c) lrows[c] += c4[q];
+    }
+  }
+  uint32_t total;
+  uint32_t pre = block_excl_scan_256(acc, &total);  // (syncs: every lcnt add is in)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t dg = t * 4u + (uint32_t)q;
+    if (dg < RAD) cnt[dg] = pre;
+    pre += c4[q];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    heads += __shfl_xor(heads, o, 64);
+    small_rows += __shfl_xor(small_rows, o, 64);
+#pragma unroll
+    for (int c = 0; c <= kBigClasses; ++c) lrows[c] += __shfl_xor(lrows[c], o, 64);
+  }
+  if (lane == 0) {
+    if (heads) atomicAdd(&lcnt[kRunLists], heads);
+    if (small_rows) atomicAdd(&lcnt[kRunLists + 1], small_rows);
+#pragma unroll
+    for (int c = 0; c <= kBigClasses; ++c)
+      if (lrows[c]) atomicAdd(&lcnt[kRunLists + 2 + c], lrows[c]);
+  }
+  __syncthreads();
+  if (t < (uint32_t)kRunRows && lcnt[t]) {  // one add per list (and counter) per bucket
+    const uint32_t v = atomicAdd(run_counter(w.rc, (int)t), lcnt[t]);
+    if (t < (uint32_t)kRunLists) lbase[t] = v;
+  }
+  if (t < (uint32_t)kRunLists) lcnt[t] = 0u;  // (reused as the list cursors)
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int l = l4[q];
+    if (l >= 0) {
+      const uint32_t dg = t * 4u + (uint32_t)q;
+      const uint32_t at = lbase[l] + atomicAdd(&lcnt[l], 1u);
+      const uint2 e = make_uint2(base + cnt[dg], c4[q]);
+      if (l < kGroupClasses) w.cls[l][at] = e;
+      else if (l < kGroupClasses + kBigClasses) w.big[l - kGroupClasses][at] = e;
+      else if (l == kRunLists - 2) w.huge[at] = e;
+      else w.over[at] = e;
+    }
+  }
+  // 3. the stable scatter, 4096 keys per round (wave wv: positions wv*1024 + j*64 + lane)
+  const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  for (uint32_t r0 = 0; r0 < m; r0 += kChunk) {
+    uint32_t k[kItems], v[kItems], lr[kItems];
+#pragma unroll
+    for (int j = 0; j < (int)kItems; ++j) {
+      const uint32_t p = r0 + wv * 1024u + (uint32_t)j * 64u + lane;
+      k[j] = p < m ? kin[base + p] : 0u;
+      v[j] = p < m ? vin[base + p] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < (int)kItems; ++j) {
+      const bool valid = r0 + wv * 1024u + (uint32_t)j * 64u + lane < m;
+      const uint32_t dig = k[j] & MASK;
+      uint64_t match = __ballot(valid);
+      for (int b = 0; b < lb; ++b) {
+        const bool bit = (dig >> b) & 1u;
+        const uint64_t mb = __ballot(bit);
+        match &= bit ? mb : ~mb;
+      }
+      const uint32_t old = wc[wv][dig];  // every lane reads before the group's leader writes
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (valid && (match & lt) == 0ull) wc[wv][dig] = old + (uint32_t)__popcll(match);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      lr[j] = old + (uint32_t)__popcll(match & lt);
+    }
+    __syncthreads();
+    for (uint32_t dg = t; dg < RAD; dg += 256) {  // wave prefixes of this round
+      const uint32_t c0 = wc[0][dg], c1 = wc[1][dg], c2 = wc[2][dg], c3 = wc[3][dg];
+      const uint32_t at = cnt[dg] + run_[dg];
+      wc[0][dg] = at;
+      wc[1][dg] = at + c0;
+      wc[2][dg] = at + c0 + c1;
+      wc[3][dg] = at + c0 + c1 + c2;
+      run_[dg] += c0 + c1 + c2 + c3;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < (int)kItems; ++j) {
+      if (r0 + wv * 1024u + (uint32_t)j * 64u + lane < m) {
+        const uint32_t o = base + wc[wv][k[j] & MASK] + lr[j];
+        kout[o] = k[j];
+        vout[o] = v[j];
+      }
+    }
+    __syncthreads();
+    for (uint32_t dg = t; dg < RAD; dg += 256) wc[0][dg] = wc[1][dg] = wc[2][dg] = wc[3][dg] = 0u;
+    __syncthreads();
   }
   kt_end(w.kt, KC_RUNS);
 }
@@ -2439,6 +2862,23 @@ struct Fork {
   }
 };
 
+// The small-run screen's margin (k_small_screen): |q~ - q_ref| <= m0 + a2 (1/|x~a| + 1/|x~b|) for
+// the screen's quotient q~ = x~a.x~b / (|x~a| |x~b|) against the reference's fl(dot / den):
+//   m0: fp16 rounding of both rows in the dot (2 * 2^-11) and in the two norms (2 * 2^-11),
+//       2^-20 for the products of the rounding errors, (4d + 16) 2^-24 for the f32 sums of the
+//       screen and of the reference (dot, |a|^2, |b|^2) and the sqrt / product / quotient roundings
+//   a2: 2^-25 per element absolute (fp16 subnormals, which gfx950 keeps in the conversion, the
+//       MFMA and v_dot2_f32_f16 under the default float mode: tools/denorm_probe.hip), summed with
+//       Cauchy-Schwarz: sqrt(d) 2^-25 (|a| + |b|) / (|a||b|), doubled (the norms' own share)
+// all times 1.5 for headroom.  Only with a fast decider (a normal s*) and the fp16 image.
+static void screen_margins(int d, float* m0, float* a2) {
+  *m0 = 1.5f * (0x1p-9f + 0x1p-20f + (4.0f * (float)d + 16.0f) * 0x1p-24f);
+  *a2 = 1.5f * 2.0f * 0x1p-25f * std::sqrt((float)d);
+}
+static bool screen_ok(const Rows& r, const Decider& dc, const MergeWork& w) {
+  return w.small_screen && r.xh && dc.fast && (r.d == 32 || r.d == 64);  // (tiles: d >= 32)
+}
+
 // The small-run merge's persistent launch (option "small_grid"; default 12288).
 static uint32_t small_grid(const MergeWork& w) {
   return w.small_grid ? std::max(256u, w.small_grid) : 12288u;
@@ -2446,12 +2886,11 @@ static uint32_t small_grid(const MergeWork& w) {
 
 // Iterations below this many positions run every merge class in ONE launch (k_merge_tail) on the
 // main stream: there the cross-stream fork/join (~35 us) costs more than the overlap buys.
-constexpr uint32_t kTailMergeMax = 1u << 20;
 
 template <int D>
 static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, const MergeWork& w,
                           Counters* ctr, uint32_t n, hipStream_t s) {
-  if (n < kTailMergeMax) {
+  if (n < tail_merge_max(w)) {
     using L896 = BigLayout<D, 896, false>;
     using L384 = BigLayout<D, 384, true>;
     using L192 = BigLayout<D, 192, true>;
@@ -2492,8 +2931,21 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   // retire and re-enter as the big-run workgroups come and go (C2, same box, interleaved:
   // 4608 -> 255.9 / 258.0 ms, 8192 -> 255.4 / 252.3, 12288 -> 250.8 / 251.7, 16384 -> 256.0 /
   // 253.9; small-run merge 79.4 -> 70.5 ms per step)
-  if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
-  k_merge_small<D><<<small_grid(w), 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
+  // the fp16 screen first (option small_screen, where the row image exists): the merge then
+  // takes only the runs it could not rule out
+  if (screen_ok(r, dc, w)) {
+    float m0, a2;
+    screen_margins(r.d, &m0, &a2);
+    const uint32_t sgrid = w.screen_grid ? std::max(64u, w.screen_grid) : 3072u;
+    k_small_screen<D><<<sgrid, 64, 0, f.lane(2)>>>(w, slots, r, dc.s_star, m0, a2, w.kt);
+    MergeWork ws = w;
+    ws.screened = 1u;
+    if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
+    k_merge_small<D><<<small_grid(w), 64, 0, f.lane(2)>>>(ws, slots, dc, r, ctr);
+  } else {
+    if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
+    k_merge_small<D><<<small_grid(w), 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
+  }
   if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[1], f.lane(2));
 }
 
@@ -2567,14 +3019,20 @@ void launch_runs(const uint32_t* key, uint32_t lo, uint32_t n, int bucket_thr, c
   }
 }
 
+void launch_tail_local(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
+                       const uint32_t* dtot, int bits, int bucket_thr, const MergeWork& w,
+                       hipStream_t s) {
+  k_tail_local<<<1024, 256, 0, s>>>(kin, vin, kout, vout, dtot, bits - 10, bucket_thr, w);
+}
+
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,
                   float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s,
-                  const uint32_t* n_dev) {
+                  const uint32_t* n_dev, bool runs_ready) {
   if (hi <= lo) return;
   const uint32_t n = hi - lo;
-  if (n_dev && (lo != 0 || n >= kTailMergeMax)) return;  // (the caller checks)
+  if (n_dev && (lo != 0 || n >= tail_merge_max(w))) return;  // (the caller checks)
   const Decider dc = make_decider(thr);
-  launch_runs(key, lo, n, bucket_thr, w, s, n_dev);
+  if (!runs_ready) launch_runs(key, lo, n, bucket_thr, w, s, n_dev);
   switch (r.d) {
     case 8: launch_groups<8>(r, slots, dc, w, ctr, n, s); break;
     case 16: launch_groups<16>(r, slots, dc, w, ctr, n, s); break;

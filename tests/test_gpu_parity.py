@@ -191,6 +191,28 @@ def test_hash_keys_packed_variant(engine, oracle):
         engine.set_option("projection", 0)
 
 
+@pytest.mark.parametrize("n,d,groups,noise", [(120000, 64, 1500, 0.05), (600000, 32, 20000, 0.05),
+                                               (200000, 16, 50, 0.01), (3000, 64, 100, 0.05),
+                                               (1048000, 8, 30000, 0.1)])
+def test_tail_local_sort_vs_oracle(engine, oracle, n, d, groups, noise):
+    """The queued small iterations' bucket sort as a top-10-bit partition + per-bucket LDS sorts
+    that list the runs (option tail_local, default) and as the LSD passes + run kernels: both
+    equal the oracle (merge_hashtable's stable order, cluster.cc:15-30), buckets over 4096 keys
+    (several LDS rounds) and keys of 11..20 bits included."""
+    rng = np.random.default_rng(n + d)
+    rows = clustered(rng, n, d, groups, noise)
+    want = oracle.cluster(rows, 0.8, 8, 1000000, 41, 9)
+    try:
+        for local in (1, 0):
+            engine.set_option("tail_local", local)
+            engine.load_rows(rows)
+            trace, counter, _ = engine.cluster(0.8, 8, 1000000, 41, 9)
+            assert np.array_equal(trace, want[3]) and counter == want[4], local
+            assert_same_result(engine.result(), *want[:3])
+    finally:
+        engine.set_option("tail_local", 1)
+
+
 @pytest.mark.parametrize("d", [64, 32])
 def test_cluster_variants_agree(engine, oracle, d):
     """Options that change the launch sequence, not the result: the queued tail batches
@@ -327,6 +349,62 @@ def test_pcluster_huge_runs_folded_vs_oracle(engine, oracle, b, d, groups, noise
     finally:
         engine.set_option("huge_fold", 0)
     assert_same_result(got, *oracle.pcluster(rows, thr))
+
+
+@pytest.mark.parametrize("d", [64, 32])
+def test_small_screen_vs_oracle(engine, oracle, d):
+    """Option small_screen: runs of 2..64 rows screened on the fp16 row image first (only the ones
+    the certified margin cannot rule out are merged on the f32 rows) — the same N_t trace, counter
+    and result bits as the oracle, with rows the image cannot screen in small runs: past fp16's
+    range, all-zero image of a nonzero row, zero, NaN."""
+    rng = np.random.default_rng(d + 7)
+    rows = clustered(rng, 150000, d, 3000, 0.05)
+    rows[5] *= np.float32(1e5)      # fp16 overflow in the image
+    rows[9, 1] = np.float32(7e4)
+    rows[11] *= np.float32(1e-9)    # image all zero
+    rows[13] = 0.0
+    rows[17, 2] = np.nan
+    want = oracle.cluster(rows, 0.8, 12, 1000000, 93, 4)
+    engine.set_option("small_screen", 1)
+    engine.set_option("tail_merge_rows", 1)  # every iteration through the per-class launches
+    try:
+        engine.load_rows(rows)
+        trace, counter, st = engine.cluster(0.8, 12, 1000000, 93, 4)
+        got = engine.result()
+    finally:
+        engine.set_option("small_screen", 0)
+        engine.set_option("tail_merge_rows", 0)
+    assert st["kern"]["screen"]["launches"] == 12
+    assert np.array_equal(trace, want[3]) and counter == want[4]
+    assert_same_result(got, *want[:3])
+
+
+@pytest.mark.parametrize("b", [2, 3, 5, 9, 17, 33, 64])
+def test_small_screen_pcluster_special_rows(engine, oracle, b):
+    """One small run through the screen (pcluster: the rows as one bucket) with a row the fp16
+    image cannot carry: ADVICE r03 (a huge row must keep its run for the exact merge)."""
+    rng = np.random.default_rng(b)
+    for special in ("huge", "tiny", "zero", "nan", "none"):
+        rows = clustered(rng, b, 64, max(1, b // 4), 0.02)
+        k = b // 2
+        if special == "huge":
+            rows[k] *= np.float32(3e4)
+        elif special == "tiny":
+            rows[k] *= np.float32(1e-9)
+        elif special == "zero":
+            rows[k] = 0.0
+        elif special == "nan":
+            rows[k, 0] = np.nan
+        engine.set_option("small_screen", 1)
+        engine.set_option("tail_merge_rows", 1)
+        try:
+            engine.load_rows(rows)
+            engine.pcluster(0.9)
+            got = engine.result()
+        finally:
+            engine.set_option("small_screen", 0)
+            engine.set_option("tail_merge_rows", 0)
+        assert_same_result(got, *oracle.pcluster(rows, 0.9)), (b, special)
 
 
 def seq_sim(a, c):
