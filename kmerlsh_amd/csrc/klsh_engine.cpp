@@ -1135,6 +1135,17 @@ static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, 
       st->sum_proj_bits += n_in * (uint64_t)h;
       st->sum_merges += n_in - cc.total;
       if (ctx->kernel_timing && ctx->kstamp) count_class_rows(st, cc, n_in, true);
+#ifdef KLSH_DIAG
+      static FILE* batch_log = [] {  // diagnostics build: the run classes of queued iterations
+        const char* e = getenv("KLSH_ITER_LOG");
+        return e ? fopen(e, "a") : nullptr;
+      }();
+      if (batch_log)
+        fprintf(batch_log, "%d %llu %d batched runs %u small_rows %u big %u %u %u %u huge %u\n",
+                ch.it0 + c, (unsigned long long)n_in, h, cc.n_seg, cc.n_small_rows, cc.n_big[0],
+                cc.n_big[1], cc.n_big[2], cc.n_big[3], cc.n_huge);
+      if (batch_log) fflush(batch_log);
+#endif
       *ctx->h_ctr = cc;
       n_known = cc.total;
     }

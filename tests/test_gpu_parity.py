@@ -351,12 +351,31 @@ def test_pcluster_huge_runs_folded_vs_oracle(engine, oracle, b, d, groups, noise
     assert_same_result(got, *oracle.pcluster(rows, thr))
 
 
-@pytest.mark.parametrize("d", [64, 32])
-def test_small_screen_vs_oracle(engine, oracle, d):
-    """Option small_screen: runs of 2..64 rows screened on the fp16 row image first (only the ones
-    the certified margin cannot rule out are merged on the f32 rows) — the same N_t trace, counter
-    and result bits as the oracle, with rows the image cannot screen in small runs: past fp16's
-    range, all-zero image of a nonzero row, zero, NaN."""
+class options:
+    """Engine options set for a block and restored to their previous values after it."""
+
+    def __init__(self, engine, **kv):
+        self.engine, self.kv, self.old = engine, kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = self.engine.get_option(k)
+            self.engine.set_option(k, v)
+        return self.engine
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            self.engine.set_option(k, v)
+        return False
+
+
+@pytest.mark.parametrize("d,screen", [(64, 1), (32, 1), (64, 0)])
+def test_small_screen_vs_oracle(engine, oracle, d, screen):
+    """Option small_screen (default 1): runs of 2..64 rows screened on the fp16 row image first
+    (only the ones the certified margin cannot rule out are merged on the f32 rows) — the same N_t
+    trace, counter and result bits as the oracle, with rows the image cannot screen in small runs:
+    past fp16's range, all-zero image of a nonzero row, zero, NaN; screen = 0: every small run
+    through the f32 merge."""
     rng = np.random.default_rng(d + 7)
     rows = clustered(rng, 150000, d, 3000, 0.05)
     rows[5] *= np.float32(1e5)      # fp16 overflow in the image
@@ -365,16 +384,12 @@ def test_small_screen_vs_oracle(engine, oracle, d):
     rows[13] = 0.0
     rows[17, 2] = np.nan
     want = oracle.cluster(rows, 0.8, 12, 1000000, 93, 4)
-    engine.set_option("small_screen", 1)
-    engine.set_option("tail_merge_rows", 1)  # every iteration through the per-class launches
-    try:
+    # tail_merge_rows = 1: every iteration through the per-class launches
+    with options(engine, small_screen=screen, tail_merge_rows=1):
         engine.load_rows(rows)
         trace, counter, st = engine.cluster(0.8, 12, 1000000, 93, 4)
         got = engine.result()
-    finally:
-        engine.set_option("small_screen", 0)
-        engine.set_option("tail_merge_rows", 0)
-    assert st["kern"]["screen"]["launches"] == 12
+    assert st["kern"]["screen"]["launches"] == 12 * screen
     assert np.array_equal(trace, want[3]) and counter == want[4]
     assert_same_result(got, *want[:3])
 
@@ -395,15 +410,10 @@ def test_small_screen_pcluster_special_rows(engine, oracle, b):
             rows[k] = 0.0
         elif special == "nan":
             rows[k, 0] = np.nan
-        engine.set_option("small_screen", 1)
-        engine.set_option("tail_merge_rows", 1)
-        try:
+        with options(engine, small_screen=1, tail_merge_rows=1):
             engine.load_rows(rows)
             engine.pcluster(0.9)
             got = engine.result()
-        finally:
-            engine.set_option("small_screen", 0)
-            engine.set_option("tail_merge_rows", 0)
         assert_same_result(got, *oracle.pcluster(rows, 0.9)), (b, special)
 
 

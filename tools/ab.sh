@@ -1,26 +1,20 @@
 #!/bin/bash
-# A/B of engine builds / environment settings on the GPU box, interleaved: one bench line per
-# setting per round.  tools/ab.sh ROUNDS "ENV=.. ENV2=.." "..." ...   ("" = the product build)
-# Extra bench flags: AB_ARGS (default: --steps 5 --warmup 1 --cpu-baseline none).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+# A/B of engine options / library variants on the C2 bench (GPU box).
+#   tools/ab.sh ROUNDS "TESTS_K" "name:lib:opts" ...   (lib empty = the default build;
+#   TESTS_K empty = no parity tests first)
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
+export TMPDIR=/tmp
 mkdir -p gpurun_out/ab
 rounds=$1; shift
-args=${AB_ARGS:---steps 5 --warmup 1 --cpu-baseline none}
-for r in $(seq 1 "$rounds"); do
-  i=0
+tk=$1; shift
+if [ -n "$tk" ]; then
+  tools/gpu_steps.sh "abtests:300:python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k '$tk'" || exit 1
+fi
+for round in $(seq 1 "$rounds"); do
   for cfg in "$@"; do
-    i=$((i + 1))
-    log=gpurun_out/ab/r${r}_$i.log
-    env $cfg timeout -k 10 300 python -u bench.py $args > $log 2>&1
-    rc=$?
-    [ $rc -eq 0 ] || { echo "[$i] $cfg rc=$rc"; tail -5 $log; exit $rc; }
-    python - "$log" "$i" "$cfg" <<'PY'
-import json, sys
-line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
-d = json.loads(line)
-ks = d["roofline"].get("kernels", [])
-top = " ".join(f"{k['class']}={k['ms_per_step']:.1f}" for k in ks[:7])
-print(f"[{sys.argv[2]}] {sys.argv[3][:44]:44s} {d['ms_per_step']:8.2f} ms parity={d['parity'].get('ok')} | {top}", flush=True)
-PY
+    name=${cfg%%:*}; rest=${cfg#*:}; lib=${rest%%:*}; opt=${rest#*:}
+    if [ -n "$lib" ]; then export KLSH_LIB=$lib; else unset KLSH_LIB; fi
+    timeout -k 10 200 python bench.py --steps 4 --warmup 1 --cpu-baseline none $opt > gpurun_out/ab/${name}_$round.log 2>&1 || { echo "$name failed"; tail -3 gpurun_out/ab/${name}_$round.log; exit 1; }
+    python3 -c "import json,sys; [print('$name $round', round(json.loads(l)['ms_per_step'],1), json.loads(l)['parity'].get('ok'), {k: round(v,1) for k,v in json.loads(l)['phases_ms_per_step'].items() if v}) for l in open('gpurun_out/ab/${name}_$round.log') if l.startswith('{')]"
   done
 done
