@@ -310,7 +310,8 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
 
     register = d in (8, 16, 32, 64)
     # shadow: the projection reads the fp16 row image (2d bytes a row; the engine keeps one at
-    # d = 16, 32, 64 unless option "projection" = 1); its close calls re-read the f32 row
+    # d = 16, 32, 64 and d > 64 with d % 8 == 0 unless option "projection" = 1 / "wide_image" = 0);
+    # its close calls re-read the f32 row
     row_bytes = 2 * d if shadow else 4 * d
     kern = {c: {f: sum(s["kern"][c][f] for s in stats) for f in ("ms", "launches", "rows", "runs")}
             for c in stats[0]["kern"]}
@@ -332,7 +333,10 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
         ach = (b / k["launches"]) / (avg * 1e-3) / 1e9
         name = (KERNEL_NAMES if register or c not in WIDE_NAMES else WIDE_NAMES)[c].format(d=d)
         if c == "project" and shadow:
-            name = f"k_project_h16<{d}>"
+            name = (f"k_project_h16<{d}>" if register
+                    else "k_project_h16_wide + k_project_fix (span)")
+        if c == "huge" and d in (16, 32):
+            name = f"k_merge_long<{d}>"
         pmc = pmc_traffic(config, c) or pmc_traffic(config, {"project": "k_project",
                                                              "small": "k_merge_small"}.get(c, ""))
         e = {"kernel": name, "class": c, "bound": "hbm", "achieved": round(ach, 2),
@@ -365,7 +369,8 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
             bits = sum(s["sum_proj_bits"] for s in stats)
             if shadow:
                 # the fp16-image screen: S = X~ (w_hi + w_lo)^T, 2 f16 MFMA products per product
-                fl = 2 * 2.0 * bits * d / k["launches"]
+                # (wide rows: a third, |x~|.|w_hi|, for the bound)
+                fl = (2 if register else 3) * 2.0 * bits * d / k["launches"]
                 e["mfma"] = {"achieved": round(fl / (avg * 1e-3) / 1e12, 2),
                              "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                              "note": "fp16 row image x w split into fp16 hi + lo on "

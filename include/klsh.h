@@ -177,12 +177,14 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *                      the ones the screen cannot rule out are merged on the f32 rows
  *   "tail_merge_rows"  iterations below this many rows merge every class in one launch (default
  *                      2^20; tests lower it to reach the per-class launches at small sizes)
- *   "h16_segcap" (tests) caps the fp16 projection's per-workgroup fix-up segment. */
+ *   "h16_segcap" (tests) caps the fp16 projection's per-workgroup fix-up segment.
+ *   "wide_image"       1 (default) = keep the fp16 row image for d > 64 too (d % 8 == 0): the
+ *                      wide projection reads it (k_project_h16_wide); 0 = the f32 rows */
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
 /* Any option above, plus read-only diagnostics: "fp16_image" (1 = the loaded rows have the fp16
  * image), "last_hash_kernel" (klsh_hash_keys' projection kernel: 0 packed chains, 1 fp16-image
- * screen, 2 bf16x3 wide-row screen, -1 none) and "last_hash_close_pairs" (its (row, hyperplane)
- * pairs settled by the exact chains). */
+ * screen, 2 f32 fp16x3 wide-row screen, 3 fp16-image wide-row screen, -1 none) and
+ * "last_hash_close_pairs" (its (row, hyperplane) pairs settled by the exact chains). */
 int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value);
 
 /* ---- results ---------------------------------------------------------------------------------- */

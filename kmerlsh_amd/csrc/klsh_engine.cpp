@@ -182,8 +182,9 @@ struct klsh_ctx {
   // option "projection" asks for the exact packed chains; every row store of the merge kernels
   // writes it too (store_row4 / store_row1)
   uint16_t* xh_alloc = nullptr;
+  bool wide_image = true;  // option "wide_image": the image for d > 64 too (k_project_h16_wide)
   bool shadow_wanted(int d_) const {
-    return pw.variant != klsh::kProjPacked && klsh::shadow_width_ok(d_);
+    return pw.variant != klsh::kProjPacked && klsh::shadow_width_ok(d_) && (d_ <= 64 || wide_image);
   }
   // Queued tail batches (run_batched; option "tail_batch", default on), their bucket sort as a
   // top-bits pass + the LDS bucket sort that lists the runs (option "tail_local", default on)
@@ -271,6 +272,8 @@ struct klsh_ctx {
     dfree(rows.nxt); dfree(order); dfree(alt); dfree(keys); dfree(keys2); dfree(nk1);
     dfree(nk2); dfree(nv2); dfree(hist); dfree(tile_sums); dfree(mw.over); dfree(mw.run_ws);
     dfree(mw.huge);
+    dfree(mw.long_P);
+    mw.long_groups = 0;
     dfree(pw.fix);
     dfree(pw.ws);
     pw.cap = 0;
@@ -321,6 +324,20 @@ struct klsh_ctx {
     stream = nullptr;
   }
 
+  // k_merge_long's bit matrices (runs over 896 rows at d = 16 / 32): one per workgroup, a
+  // workgroup per 897 slots up to 256 (2 MB each)
+  int ensure_long(uint64_t s, int d_) {
+    const uint32_t want =
+        klsh::long_ok(d_) && s >= 897 ? (uint32_t)std::min<uint64_t>(256, s / 897 + 1) : 0u;
+    if (want <= mw.long_groups) return 0;
+    dfree(mw.long_P);
+    mw.long_groups = 0;
+    if (int e = dalloc(&mw.long_P, (size_t)want * klsh::kLongRows * (klsh::kLongRows / 64)))
+      return e;
+    mw.long_groups = want;
+    return 0;
+  }
+
   // (Re)allocate device state for `ns` slots, `nm` member nodes, row width d.
   int reserve(uint64_t ns, uint64_t nm, int d_) {
     if (ns >= 0xFFFFFFF0ull || nm >= 0xFFFFFFF0ull) return fail(KLSH_E_RANGE, "rows >= 2^32");
@@ -333,7 +350,7 @@ struct klsh_ctx {
       rows.dp = dp;
       rows.xh = shadow_wanted(d) ? xh_alloc : nullptr;
       drop_snapshot();
-      return 0;
+      return ensure_long(cap_slots, d_);
     }
     release_state();
     const uint64_t s = std::max<uint64_t>(ns, 1), m = std::max<uint64_t>(nm, 1);
@@ -358,6 +375,10 @@ struct klsh_ctx {
         release_state();
         return e;
       }
+    }
+    if ((e = ensure_long(s, d_))) {
+      release_state();
+      return e;
     }
     for (int c = 0; c < klsh::kGroupClasses; ++c) {
       if ((e = dalloc(&mw.cls[c], klsh::group_class_capacity(c, s))) ||
@@ -1750,6 +1771,12 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->pw.variant = (uint32_t)value;
     return ctx->apply_projection_variant();
   }
+  if (n == "wide_image") {
+    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_image must be 0 or 1");
+    KLSH_HIP(hipSetDevice(ctx->device));
+    ctx->wide_image = value != 0;
+    return ctx->apply_projection_variant();
+  }
   if (n == "comm_timeout_s") {
     if (value <= 0) return fail(KLSH_E_ARG, "comm_timeout_s must be > 0");
     ctx->comm_timeout_s = (double)value;
@@ -1802,6 +1829,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "small_screen_grid") *value = ctx->mw.screen_grid;
   else if (n == "tail_merge_rows") *value = klsh::tail_merge_max(ctx->mw);
   else if (n == "small_screen") *value = ctx->mw.small_screen;
+  else if (n == "wide_image") *value = ctx->wide_image;
   else if (n == "fp16_image") *value = ctx->rows.xh != nullptr;
   else if (n == "last_hash_kernel") *value = ctx->last_hash_kernel;
   else if (n == "last_hash_close_pairs") *value = (int64_t)ctx->last_hash_close;

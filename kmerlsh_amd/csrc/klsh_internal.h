@@ -148,6 +148,10 @@ struct MergeWork {
   // their own (set after several iterations without such runs: C2 and C5 never have any, and an
   // empty launch still costs its dispatch; C4, where they recur, keeps the 512-lane kernel)
   uint32_t huge_fold;
+  // runs over 896 rows at d = 16 / 32 (k_merge_long): each workgroup's bit matrix, kLongRows x
+  // kLongRows / 64 words, and the number of workgroups it has room for (0: k_merge_huge)
+  uint64_t* long_P;
+  uint32_t long_groups;
   // launch sizes (klsh_set_option; 0 = the measured default, see the launch code)
   uint32_t small_grid;       // "small_grid": the small-run merge's persistent launch
   uint32_t tail_nbig;        // "tail_big_groups": k_merge_tail's big-run workgroups
@@ -165,6 +169,8 @@ struct MergeWork {
   hipEvent_t join[3];
 };
 constexpr int kMergeStreams = 3;
+constexpr uint32_t kLongRows = 4096;  // the longest run k_merge_long walks (longer: k_merge_huge)
+inline bool long_ok(int d) { return d == 16 || d == 32; }
 inline uint32_t tail_merge_max(const MergeWork& w) { return w.tail_max ? w.tail_max : (1u << 20); }
 
 // Row state, structure-of-arrays, one entry per slot (a slot is a row of the loaded matrix;
@@ -185,7 +191,9 @@ struct Rows {
   uint16_t* xh = nullptr;
 };
 // The fp16 image is kept for these widths (the matrix-core screen takes 16 columns per step).
-inline bool shadow_width_ok(int d) { return d == 16 || d == 32 || d == 64; }
+// widths that keep the fp16 row image: the register projections' (16, 32, 64) and wide rows whose
+// image rows are 16-B aligned (d > 64, a multiple of 8: k_project_h16_wide)
+inline bool shadow_width_ok(int d) { return d == 16 || d == 32 || d == 64 || (d > 64 && d % 8 == 0); }
 
 // The merge test of cluster.cc:68-69 as a threshold on the quotient.  The reference computes
 // sim = dot / (sqrtf(|a|^2) * sqrtf(|b|^2)); dist = 1 - sim; and merges when 1 - dist >= thr.
@@ -247,7 +255,7 @@ void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* key
 
 // pw (may be null): the workspace that enables the matrix-core screens (the fp16 row image where
 // r.xh is set, bf16x3 for d > 64).  Returns the kernel it launched (ProjKernel).
-enum ProjKernel : int { kPkNone = -1, kPkPacked = 0, kPkH16 = 1, kPkWide = 2 };
+enum ProjKernel : int { kPkNone = -1, kPkPacked = 0, kPkH16 = 1, kPkWide = 2, kPkWideH16 = 3 };
 int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
                    const float* W, int h, uint32_t key_or, hipStream_t s,
                    const ProjectWork* pw = nullptr, KTime kt = kNoTime);

@@ -1343,7 +1343,8 @@ __device__ __forceinline__ void split8(const float* p, bool ok, bf16x8& hi, bf16
 // P[c] bit a).  rowA(a) / rowB(c) give the rows (LDS or memory); D = d, a multiple of 16.
 template <int D, class RowA, class RowB>
 __device__ __forceinline__ void gram_tile(uint32_t R, uint32_t C, uint32_t b, RowA rowA, RowB rowB,
-                                          const float* sq, const Decider& dc, uint64_t* P, int W) {
+                                          const float* sq, const Decider& dc, uint64_t* P, int W,
+                                          uint32_t* fb = nullptr) {
   const uint32_t lane = __lane_id(), r = lane & 31u, h = lane >> 5;
   const uint32_t a0 = R * 64u, c0 = C * 64u;
   f32x16 acc[2][2];
@@ -1430,7 +1431,11 @@ __device__ __forceinline__ void gram_tile(uint32_t R, uint32_t C, uint32_t b, Ro
       if (lane == r0 + 4u) own = w1;
     }
   }
-  if (own && a0 + lane < b) atomicOr((unsigned long long*)&P[(a0 + lane) * W + C], (unsigned long long)own);
+  if (own && a0 + lane < b) {
+    atomicOr((unsigned long long*)&P[(a0 + lane) * W + C], (unsigned long long)own);
+    // fb (k_merge_long): row a's first match below it, over every column block
+    if (fb) atomicMin(&fb[a0 + lane], C * 64u + (uint32_t)__builtin_ctzll(own));
+  }
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
     const uint64_t full = tmask[n] | shfl64(tmask[n], lane ^ 32u);
@@ -2414,9 +2419,436 @@ static size_t huge_lds(int d, int dp, int nt) {
                   : sizeof(float) * (size_t)dp);
 }
 
+// ------------------------------------- runs over 896 rows: Gram bit matrix + one step per merge -----
+// k_merge_long<D> (d = 16 or 32, a decider with a fast path): one 512-lane workgroup per run of up
+// to kLongRows rows (longer runs keep huge_runs, in the same launch).  huge_runs pays a pass over
+// the run for every 4-8 visited rows whether they merge or not (C4: 1.2K-row runs with ~12 % of
+// their rows merging, 4.6 ms of walk each); here
+//  1. every decision of the run comes from the certified MFMA Gram tiles (gram_tile; exact chains
+//     for the close calls) into a position-space bit matrix in global memory (w.long_P, b words
+//     of ceil(b/64) per row, up to 2 MB per workgroup; P[y] bit q = decide(row y, row at q)), and
+//     fb[q], the first position below q that q matches, from the same tiles;
+//  2. the walk then costs one step per MERGE: the lowest position q >= i with a match (one 64-bit
+//     word per wave in LDS and one barrier), the consensus into its first match j, the last
+//     position's row moved into i, and every position still to be visited re-decides its bit j
+//     against the new row (short chains + the certified pre-screen, exact chains for the close
+//     calls), takes its bit i from the moved row's matrix row (symmetric; untouched above i),
+//     stores both bits (atomics) and updates its fb from them — rescanning its row of the matrix
+//     only when its first match was one of the two and is gone.
+// Lane t owns positions t + 512k: the rows of the first LongRegs<D>::KP of them stay in registers
+// (a row at a position >= i never changes; the row moved into i comes from an LDS copy that the
+// owner of the last position keeps), the rest are read from memory per step.
+constexpr int kLongNT = 512;
+constexpr uint32_t kLongWords = kLongRows / 64;  // matrix words per row at the longest run
+template <int D>
+struct LongRegs {
+  static constexpr int KP = 0;
+};
+template <>
+struct LongRegs<16> {
+  static constexpr int KP = 8;
+};
+template <>
+struct LongRegs<32> {
+  static constexpr int KP = 3;
+};
+static size_t long_lds() { return sizeof(uint32_t) * kLongRows * 7; }
+
+// k_merge_long's global-memory hand-offs between waves: the matrix words are updated by atomics
+// (performed in L2) and read back by other waves, and rewritten rows are read by every wave, so
+// reads bypass the CU's L1 (agent-scope loads) and every barrier that publishes such writes first
+// waits for them (__syncthreads alone does not wait for outstanding vector-memory writes).
+__device__ __forceinline__ uint64_t ld_l2(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_l2(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void vm_barrier() {
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+  __syncthreads();
+}
+
+// First set bit of the matrix row Py in [lo, hi), with bit j taken as dn and bit i (kNone: none)
+// as bm — this step's two stores may not have landed yet.  Rare (a first match that is gone).
+__device__ __noinline__ uint32_t long_rescan(const uint64_t* Py, uint32_t lo, uint32_t hi, uint32_t j,
+                                             bool dn, uint32_t i, bool bm) {
+  const uint64_t bj = 1ull << (j & 63u), bi = 1ull << (i & 63u);
+  for (uint32_t k = lo >> 6; k * 64u < hi; ++k) {
+    uint64_t wd = ld_l2(Py + k);
+    if (k == (j >> 6)) wd = dn ? (wd | bj) : (wd & ~bj);
+    if (i != 0xFFFFFFFFu && k == (i >> 6)) wd = bm ? (wd | bi) : (wd & ~bi);
+    if (k == (lo >> 6)) wd &= ~0ull << (lo & 63u);
+    if (hi - k * 64u < 64u) wd &= (1ull << (hi - k * 64u)) - 1ull;
+    if (wd) return k * 64u + (uint32_t)__builtin_ctzll(wd);
+  }
+  return 0xFFFFFFFFu;
+}
+
+// One position of k_merge_long past the register ones: its row from memory against the new row
+// (short chains + pre-screen, the sequential chains for a close call); the row copied to `last`
+// if given.  Out of line: the register positions' rows stay live around the call.
+template <int D>
+__device__ __noinline__ uint32_t long_mem_decide(const float* xp, const float* cw, float sy,
+                                                 float sc_a, Decider dc, float* last) {
+  float d4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int k = 0; k < D; k += 4) {
+    const float4 u = *reinterpret_cast<const float4*>(cw + k);
+    const float4 xv = *reinterpret_cast<const float4*>(xp + k);
+    d4[0] = d4[0] + xv.x * u.x;
+    d4[1] = d4[1] + xv.y * u.y;
+    d4[2] = d4[2] + xv.z * u.z;
+    d4[3] = d4[3] + xv.w * u.w;
+  }
+  uint32_t v = prescreen(dc, (d4[0] + d4[1]) + (d4[2] + d4[3]), sy * sc_a);
+  if (v == 2u) {
+    float nn = 0.0f, dot = 0.0f;
+    for (int k = 0; k < D; ++k) nn = nn + cw[k] * cw[k];
+    for (int k = 0; k < D; ++k) dot = dot + xp[k] * cw[k];
+    v = decide(dc, dot, sy * __builtin_sqrtf(nn)) ? 1u : 0u;
+  }
+  if (last)
+    for (int k = 0; k < D; ++k) last[k] = xp[k];
+  return v;
+}
+
+template <int D>
+__device__ __forceinline__ void long_run(uint32_t p, uint32_t b, uint64_t* __restrict__ P,
+                                         uint32_t* __restrict__ slots, const Decider& dc,
+                                         const Rows& r, const MergeWork& w, Counters* ctr,
+                                         unsigned char* smem) {
+  constexpr int NT = kLongNT, NW = NT / 64;
+  constexpr int KR = LongRegs<D>::KP;               // positions per lane with the row in registers
+  constexpr int KT = (int)(kLongRows / (uint32_t)NT);  // positions per lane
+  constexpr uint32_t CT = kLongRows;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  constexpr uint64_t kNone64 = ~0ull;
+  static_assert(KR > 0 && KR <= KT && CT <= 4096, "positions are packed in 12 bits");
+  uint32_t* slot = reinterpret_cast<uint32_t*>(smem);  // by row id
+  uint32_t* cnt = slot + CT;
+  uint32_t* hd = slot + 2 * CT;
+  uint32_t* tl = slot + 3 * CT;
+  uint32_t* pos2row = slot + 4 * CT;
+  float* sq = reinterpret_cast<float*>(slot + 5 * CT);  // sqrtf(nrm), distance.cc:37
+  uint32_t* fb = slot + 6 * CT;                          // by POSITION
+  __shared__ __attribute__((aligned(16))) float cwall[NW][D];  // each wave's copy of the new row
+  __shared__ __attribute__((aligned(16))) float lrow[2][D];    // the row at the last position
+  __shared__ uint64_t wbuf[2][NW];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t W = (b + 63u) >> 6;
+  const int dp = r.dp;
+  [[maybe_unused]] const uint64_t pt0 = MPROF_T();
+  // 1. metadata in LDS, the matrix zeroed
+  for (uint32_t a = t; a < b; a += NT) {
+    const uint32_t s = slots[p + a];
+    slot[a] = s;
+    cnt[a] = r.cnt[s];
+    hd[a] = r.head[s];
+    tl[a] = r.tail[s];
+    pos2row[a] = a;
+    sq[a] = __builtin_sqrtf(r.nrm[s]);
+    fb[a] = kNone;
+  }
+  {
+    uint4* P4 = reinterpret_cast<uint4*>(P);
+    const uint32_t n4 = (b * W + 1u) / 2u;  // (one word past b * W at most: inside the block)
+    for (uint32_t q = t; q < n4; q += NT) P4[q] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  vm_barrier();  // (the zeros are in L2 before any tile's atomics)
+  // 2. every decision of the run, and each position's first match below it
+  {
+    auto rm = [&](uint32_t a) -> const float* { return r.x + (size_t)slot[a] * dp; };
+    const uint32_t ntiles = W * (W + 1u) / 2u;
+    for (uint32_t ti = wv; ti < ntiles; ti += NW) {
+      uint32_t R = (uint32_t)((__builtin_sqrtf(8.0f * (float)ti + 1.0f) - 1.0f) * 0.5f);
+      while (R * (R + 1u) / 2u > ti) --R;
+      while ((R + 1u) * (R + 2u) / 2u <= ti) ++R;
+      gram_tile<D>(R, ti - R * (R + 1u) / 2u, b, rm, rm, sq, dc, P, (int)W, fb);
+    }
+  }
+  vm_barrier();
+  [[maybe_unused]] const uint64_t pt1 = MPROF_T();
+  // 3. the walk
+  float xr[KR][D];  // rows of my register positions t + kp * NT
+#pragma unroll
+  for (int kp = 0; kp < KR; ++kp) {
+    const uint32_t q = t + (uint32_t)kp * NT;
+    if (q < b) {
+      load_row<D>(r.x + (size_t)slot[q] * dp, xr[kp]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) xr[kp][k] = 0.0f;
+    }
+  }
+  // a hit: position (12 bits) | its first match | its row | the row at the first match
+  auto pack = [](uint32_t q, uint32_t j, uint32_t y, uint32_t c) -> uint64_t {
+    return ((uint64_t)q << 36) | ((uint64_t)j << 24) | ((uint64_t)y << 12) | (uint64_t)c;
+  };
+  auto publish = [&](uint32_t par, uint64_t mine) {  // the wave's lowest hit -> wbuf[par][wv]
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine = min(mine, shfl64(mine, lane ^ (uint32_t)o));
+    if (lane == 0) wbuf[par][wv] = mine;
+  };
+  auto put_last = [&](uint32_t buf, const float (&x)[D]) {
+#pragma unroll
+    for (int k = 0; k < D; k += 4)
+      *reinterpret_cast<float4*>(&lrow[buf][k]) = make_float4(x[k], x[k + 1], x[k + 2], x[k + 3]);
+  };
+  uint32_t size = b, par = 0, lp = 0;
+  {
+    uint64_t mine = kNone64;
+    for (uint32_t q = t; q < b; q += NT) {
+      const uint32_t f = fb[q];
+      if (q >= 1u && f != kNone) mine = min(mine, pack(q, f, q, f));
+    }
+    publish(0, mine);
+    const uint32_t ql = b - 1u;  // the last position's row
+    if (t == ql % NT) {
+      float xl[D];
+      load_row<D>(r.x + (size_t)slot[ql] * dp, xl);
+      put_last(0, xl);
+    }
+  }
+  __syncthreads();
+  bool have = false;
+  uint32_t ip = 0, mp = 0, cp = 0, rp = 0, cntp = 0, hdp = 0;
+  [[maybe_unused]] uint64_t steps = 0;
+  while (true) {
+    uint64_t best = kNone64;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) best = min(best, wbuf[par][q]);
+    par ^= 1u;
+    if (have) {  // the previous step's writes to the shared state, by every wave before its reads
+      if (lane == 0) {
+        pos2row[ip] = mp;
+        cnt[cp] = cntp;
+        cnt[rp] = 0u;
+        hd[cp] = hdp;
+      }
+      wave_lds_fence();
+    }
+    if (best == kNone64) break;
+    ++steps;
+    // (wave-uniform values: scalar registers)
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(best >> 32));
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)best);
+    const uint32_t i = hi32 >> 4, j = ((hi32 & 15u) << 8) | (lo32 >> 24),
+                   rr = (lo32 >> 12) & 0xFFFu, c = lo32 & 0xFFFu;
+    const uint32_t last = size - 1u;
+    const uint32_t moved = __builtin_amdgcn_readfirstlane(pos2row[last]);  // (rr if i is last)
+    const uint32_t ca = __builtin_amdgcn_readfirstlane(cnt[rr]),
+                   cb = __builtin_amdgcn_readfirstlane(cnt[c]),
+                   hr = __builtin_amdgcn_readfirstlane(hd[rr]),
+                   tr = __builtin_amdgcn_readfirstlane(tl[rr]),
+                   hc = __builtin_amdgcn_readfirstlane(hd[c]);
+    const uint32_t s_r = __builtin_amdgcn_readfirstlane(slot[rr]),
+                   s_c = __builtin_amdgcn_readfirstlane(slot[c]);
+    const uint32_t f_last = __builtin_amdgcn_readfirstlane(fb[last]);
+    // the moved row's matrix row: its bits at the positions above i are the Gram tiles' own
+    const uint64_t pm = lane < W ? ld_l2(P + (size_t)moved * W + lane) : 0ull;
+    // consensus (funcAB.cc:65), current row first, into this wave's copy of the new row c
+    const float fa = (float)(int)ca, fbc = (float)(int)cb, fn = (float)(int)(ca + cb);
+    if (lane < (uint32_t)D) {
+      const float v = consensus(ld_l2(r.x + (size_t)s_r * dp + lane), fa,
+                                ld_l2(r.x + (size_t)s_c * dp + lane), fbc, fn);
+      cwall[wv][lane] = v;
+      if (wv == 0) store_row1(r, (size_t)s_c * dp + lane, v);
+    }
+    if (t == 0) r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
+    wave_lds_fence();
+    size = last;  // swap-remove: the row at the old last position moves to i
+    const float* cw = &cwall[wv][0];
+    float n4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < D; k += 4) {
+      const float4 u = *reinterpret_cast<const float4*>(cw + k);
+      n4[0] = n4[0] + u.x * u.x;
+      n4[1] = n4[1] + u.y * u.y;
+      n4[2] = n4[2] + u.z * u.z;
+      n4[3] = n4[3] + u.w * u.w;
+    }
+    const float sc_a = __builtin_sqrtf((n4[0] + n4[1]) + (n4[2] + n4[3]));
+    uint64_t mine = kNone64;
+    // position q >= i (row y) with bit j re-decided (dn) and bit i taken (bm): store both bits,
+    // update fb[q], offer a hit
+    auto settle = [&](uint32_t q, uint32_t y, bool dn, bool bm) {
+      uint64_t* Py = P + (size_t)y * W;
+      const uint64_t bj = 1ull << (j & 63u), bi = 1ull << (i & 63u);
+      if (dn) atomicOr((unsigned long long*)&Py[j >> 6], (unsigned long long)bj);
+      else atomicAnd((unsigned long long*)&Py[j >> 6], (unsigned long long)~bj);
+      uint32_t f;
+      bool lost;
+      uint32_t lower;
+      if (q == i) {  // the moved row: below i only bit j changed
+        f = f_last < i ? f_last : kNone;
+        lost = f == j && !dn;
+        lower = dn ? j : kNone;
+      } else {
+        if (bm) atomicOr((unsigned long long*)&Py[i >> 6], (unsigned long long)bi);
+        else atomicAnd((unsigned long long*)&Py[i >> 6], (unsigned long long)~bi);
+        f = fb[q];
+        lost = (f == j && !dn) || (f == i && !bm);
+        lower = dn ? j : (bm ? i : kNone);
+      }
+      if (!lost) {
+        f = min(f, lower);
+      } else if (lower < f) {
+        f = lower;
+      } else {  // the first match is gone: the unchanged bits between it and `lower`
+        const uint32_t g = long_rescan(Py, f + 1u, min(lower, q), j, dn, q != i ? i : kNone, bm);
+        f = g != kNone ? g : lower;
+      }
+      fb[q] = f;
+      if (f != kNone) mine = min(mine, pack(q, f, y, f == i ? moved : pos2row[f]));
+    };
+    // the register positions: decisions first (rows live), then the bookkeeping (rows dead)
+    uint32_t dmask = 0u;
+#pragma unroll
+    for (int kp = 0; kp < KR; ++kp) {
+      const uint32_t q = t + (uint32_t)kp * NT;
+      if (q >= i && q < size) {
+        const uint32_t y = q == i ? moved : pos2row[q];
+        const float sy = sq[y];
+        if (q == i) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) xr[kp][k] = lrow[lp][k];
+        }
+        float d4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < D; k += 4) {
+          const float4 u = *reinterpret_cast<const float4*>(cw + k);
+          d4[0] = d4[0] + xr[kp][k] * u.x;
+          d4[1] = d4[1] + xr[kp][k + 1] * u.y;
+          d4[2] = d4[2] + xr[kp][k + 2] * u.z;
+          d4[3] = d4[3] + xr[kp][k + 3] * u.w;
+        }
+        uint32_t v = prescreen(dc, (d4[0] + d4[1]) + (d4[2] + d4[3]), sy * sc_a);
+        if (v == 2u) {  // rare: the reference's sequential chains (distance.cc:27-38)
+          float nn = 0.0f, dot = 0.0f;
+#pragma unroll
+          for (int k = 0; k < D; ++k) nn = nn + cw[k] * cw[k];
+#pragma unroll
+          for (int k = 0; k < D; ++k) dot = dot + xr[kp][k] * cw[k];
+          v = decide(dc, dot, sy * __builtin_sqrtf(nn)) ? 1u : 0u;
+        }
+        dmask |= v << kp;
+        if (q == size - 1u) put_last(lp ^ 1u, xr[kp]);  // the next swap-remove's row
+      }
+      asm volatile("" ::: "memory");  // (the new row is re-read from LDS per position)
+    }
+#pragma unroll
+    for (int kp = 0; kp < KR; ++kp) {
+      const uint32_t q = t + (uint32_t)kp * NT;
+      // bit i of row q := decide(q, moved) = the moved row's bit q (wave-uniform shuffle)
+      const uint64_t wm = shfl64(pm, (q >> 6) & 63u);
+      const bool bm = (wm >> (q & 63u)) & 1ull;
+      if (q >= i && q < size) settle(q, q == i ? moved : pos2row[q], (dmask >> kp) & 1u, bm);
+    }
+#pragma unroll 1
+    for (int kp = KR; kp < KT; ++kp) {  // positions past them (runs over KR * 512 rows): memory
+      const uint32_t q = t + (uint32_t)kp * NT;
+      const uint64_t wm = shfl64(pm, (q >> 6) & 63u);
+      const bool bm = (wm >> (q & 63u)) & 1ull;
+      if (q >= i && q < size) {
+        const uint32_t y = q == i ? moved : pos2row[q];
+        const float* xp = r.x + (size_t)slot[y] * dp;
+        const uint32_t v = long_mem_decide<D>(xp, cw, sq[y], sc_a, dc, q == size - 1u ? &lrow[lp ^ 1u][0] : nullptr);
+        settle(q, y, v != 0u, bm);
+      }
+    }
+    publish(par, mine);
+    have = true;
+    ip = i;
+    mp = moved;
+    cp = c;
+    rp = rr;
+    cntp = ca + cb;
+    hdp = hr;
+    lp ^= 1u;
+    vm_barrier();  // this step's matrix bits and the new row are in L2
+  }
+  vm_barrier();
+  // write back: survivors in position order, kInvalid after; rewritten rows' norms and metadata
+  for (uint32_t q = t; q < b; q += NT) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
+  for (uint32_t q0 = 0; q0 < size; q0 += NT) {  // uniform trip count (ballot inside)
+    const uint32_t q = q0 + t;
+    bool rewritten = false;
+    uint32_t s = 0;
+    if (q < size) {
+      const uint32_t y = pos2row[q];
+      s = slot[y];
+      rewritten = r.cnt[s] != cnt[y];  // every merge into a row raises its count
+      if (rewritten) {  // the exact sequential norm of the new row (distance.cc:33-34)
+        float xv[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) xv[k] = ld_l2(r.x + (size_t)s * dp + k);
+        float nv = 0.0f;
+#pragma unroll
+        for (int k = 0; k < D; ++k) nv = nv + xv[k] * xv[k];
+        r.nrm[s] = nv;
+        r.cnt[s] = cnt[y];
+        r.head[s] = hd[y];
+      }
+    }
+    if (w.dlist) append_slot(rewritten, s, w.dlist, &ctr->n_delta);
+  }
+  __syncthreads();
+#ifdef KLSH_MERGE_PROF
+  if (t == 0) {
+    const uint64_t pt2 = MPROF_T();
+    MPROF_ADD(kBigClasses, 0, 1);
+    MPROF_ADD(kBigClasses, 1, b);
+    MPROF_ADD(kBigClasses, 2, b - size);
+    MPROF_ADD(kBigClasses, 3, pt1 - pt0);
+    MPROF_ADD(kBigClasses, 4, pt2 - pt1);
+    MPROF_MAX(kBigClasses, 5, pt2 - pt0);
+    MPROF_MAX(kBigClasses, 6, b);
+  }
+#endif
+}
+
+template <int D>
+__global__ __launch_bounds__(kLongNT) void k_merge_long(const uint2* __restrict__ list,
+                                                        const uint32_t* count_ptr,
+                                                        uint32_t* __restrict__ slots, Decider dc,
+                                                        Rows r, MergeWork w, Counters* ctr) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  kt_begin(w.kt, KC_HUGE);
+  const uint32_t count = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t* P = w.long_P + (size_t)blockIdx.x * kLongRows * kLongWords;
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {  // block-uniform
+    const uint2 e = list[li];
+    if (e.y <= kLongRows) long_run<D>(e.x, e.y, P, slots, dc, r, w, ctr, smem);
+    else huge_runs<D, kLongNT>(list, li + 1u, li, 1u << 30, slots, dc, r, w, ctr, smem);
+    __syncthreads();
+  }
+  kt_end(w.kt, KC_HUGE);
+}
+
 static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, const Rows& r,
                         Counters* ctr, uint32_t n, hipStream_t s) {
   if (w.huge_fold) return;  // the 385..896-row kernel walks them (k_merge_big)
+  uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
+  if (w.huge_cap) g = std::min(g, w.huge_cap);  // (the kernel strides over its list)
+  if (w.long_P && w.long_groups && dc.fast && (r.d == 16 || r.d == 32)) {
+    const size_t lds = std::max(long_lds(), huge_lds(r.d, r.dp, kLongNT));
+    static const bool lds_ok = [lds] {
+      bool ok = true;
+      for (const void* f : {reinterpret_cast<const void*>(&k_merge_long<16>),
+                            reinterpret_cast<const void*>(&k_merge_long<32>)})
+        ok = ok && hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) ==
+                       hipSuccess;
+      return ok;
+    }();
+    (void)lds_ok;
+    g = std::min(g, w.long_groups);
+    if (r.d == 16)
+      k_merge_long<16><<<g, kLongNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr);
+    else
+      k_merge_long<32><<<g, kLongNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr);
+    return;
+  }
   const size_t lds = huge_lds(r.d, r.dp, kHugeNT);
   static const bool lds_ok = [] {
     bool ok = true;
@@ -2430,8 +2862,6 @@ static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, 
     return ok;
   }();
   (void)lds_ok;
-  uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
-  if (w.huge_cap) g = std::min(g, w.huge_cap);  // (the kernel strides over its list)
   switch (r.d) {
     case 8: k_merge_huge<8><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr); break;
     case 16: k_merge_huge<16><<<g, kHugeNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr); break;

@@ -139,22 +139,27 @@ def adversarial_rows(rng, n, d, w):
     return rows
 
 
-@pytest.mark.parametrize("d,h", [(64, 23), (32, 18), (16, 9), (64, 31), (32, 1), (8, 7),
-                                 (512, 20), (100, 31), (72, 5)])
-def test_hash_keys_close_calls_vs_oracle(engine, oracle, d, h):
-    """The loop's projection kernels (klsh_hash_keys uses the same dispatch and, at d = 16/32/64,
-    the fp16 row image) on adversarial rows, bit-equal to the reference's sequential chains
-    (hash/lshash.cc:44-59: s == +0/-0 -> 1, tiny negative -> 0, NaN -> 0).  The screen runs and
-    leaves close calls to the exact chains, which the test asserts."""
+@pytest.mark.parametrize("d,h,wide_image", [(64, 23, 1), (32, 18, 1), (16, 9, 1), (64, 31, 1),
+                                            (32, 1, 1), (8, 7, 1), (512, 20, 1), (512, 20, 0),
+                                            (100, 31, 1), (72, 5, 1), (72, 5, 0), (136, 32, 1)])
+def test_hash_keys_close_calls_vs_oracle(engine, oracle, d, h, wide_image):
+    """The loop's projection kernels (klsh_hash_keys uses the same dispatch and the fp16 row image
+    at d = 16/32/64 and at d > 64 with d % 8 == 0: k_project_h16_wide; wide_image = 0 or
+    d = 100: the f32 fp16x3 screen) on adversarial rows, bit-equal to the reference's sequential
+    chains (hash/lshash.cc:44-59: s == +0/-0 -> 1, tiny negative -> 0, NaN -> 0).  The screen
+    runs and leaves close calls to the exact chains, which the test asserts."""
     from kmerlsh_amd import _native
 
     rng = np.random.default_rng(11 + d + h)
     w, _ = _native.hyperplanes(7 + d, 0, h, d)
     rows = adversarial_rows(rng, 4000, d, w)
-    got = engine.hash_keys(rows, w)
+    with options(engine, wide_image=wide_image):
+        got = engine.hash_keys(rows, w)
+        kern = engine.get_option("last_hash_kernel")
     assert np.array_equal(got, oracle.keys(rows, w)), (d, h)
-    kern = engine.get_option("last_hash_kernel")
-    assert kern == {16: 1, 32: 1, 64: 1, 8: 0}.get(d, 2), kern  # fp16 screen / packed / bf16x3
+    # fp16 screen / packed / f32 fp16x3 wide screen / fp16-image wide screen
+    want = {16: 1, 32: 1, 64: 1, 8: 0}.get(d, 3 if wide_image and d % 8 == 0 else 2)
+    assert kern == want, kern
     if kern:
         assert engine.get_option("last_hash_close_pairs") > 0
 
@@ -390,6 +395,61 @@ def test_small_screen_vs_oracle(engine, oracle, d, screen):
         trace, counter, st = engine.cluster(0.8, 12, 1000000, 93, 4)
         got = engine.result()
     assert st["kern"]["screen"]["launches"] == 12 * screen
+    assert np.array_equal(trace, want[3]) and counter == want[4]
+    assert_same_result(got, *want[:3])
+
+
+@pytest.mark.parametrize("b,d,groups,noise,thr", [
+    (897, 32, 60, 0.05, 0.9), (1000, 16, 1000, 0.3, 0.99), (1536, 32, 100, 0.05, 0.9),
+    (1537, 32, 100, 0.05, 0.9), (2048, 16, 150, 0.05, 0.9), (3000, 32, 300, 0.08, 0.85),
+    (4096, 32, 50, 0.03, 0.95), (4097, 32, 400, 0.05, 0.9), (2500, 32, 2, 0.01, 0.9),
+    (1800, 16, 1800, 0.5, 0.999), (1300, 32, 20, 0.2, 0.8)])
+def test_long_runs_vs_oracle(engine, oracle, b, d, groups, noise, thr):
+    """Runs over 896 rows through k_merge_long (d = 16, 32: the Gram bit matrix in memory, one
+    walk step per merge; rows past 1536 / 2048 positions read from memory; over 4096 rows:
+    huge_runs in the same launch): merge-dense and merge-sparse, every length boundary."""
+    rng = np.random.default_rng(b * 11 + d)
+    rows = clustered(rng, b, d, groups, noise)
+    with options(engine, tail_merge_rows=1):  # the per-class launches, not k_merge_tail
+        engine.load_rows(rows)
+        engine.pcluster(thr)
+        got = engine.result()
+    assert_same_result(got, *oracle.pcluster(rows, thr))
+
+
+@pytest.mark.parametrize("special", ["nan", "zero", "huge", "tiny"])
+def test_long_runs_special_rows(engine, oracle, special):
+    """A long run with a row the pre-screen cannot call (NaN, zero, 1e30, 1e-30 scale): the
+    exact chains decide it, in the Gram tiles and in the walk."""
+    rng = np.random.default_rng(5)
+    rows = clustered(rng, 1200, 32, 80, 0.05)
+    k = 600
+    if special == "nan":
+        rows[k, 3] = np.nan
+    elif special == "zero":
+        rows[k] = 0.0
+    elif special == "huge":
+        rows[k] *= np.float32(1e30)
+    else:
+        rows[k] *= np.float32(1e-30)
+    with options(engine, tail_merge_rows=1):
+        engine.load_rows(rows)
+        engine.pcluster(0.9)
+        got = engine.result()
+    assert_same_result(got, *oracle.pcluster(rows, 0.9))
+
+
+def test_long_runs_in_the_loop_vs_oracle(engine, oracle):
+    """The cluster loop with buckets over 896 rows every iteration (few tight groups at d = 32):
+    same N_t trace, counter and result as the oracle."""
+    rng = np.random.default_rng(77)
+    rows = clustered(rng, 30000, 32, 12, 0.03)
+    want = oracle.cluster(rows, 0.8, 6, 1000000, 41, 4)
+    with options(engine, tail_merge_rows=1):
+        engine.load_rows(rows)
+        trace, counter, st = engine.cluster(0.8, 6, 1000000, 41, 4)
+        got = engine.result()
+    assert st["kern"]["huge"]["launches"] > 0
     assert np.array_equal(trace, want[3]) and counter == want[4]
     assert_same_result(got, *want[:3])
 
