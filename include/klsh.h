@@ -178,8 +178,10 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *   "tail_merge_rows"  iterations below this many rows merge every class in one launch (default
  *                      2^20; tests lower it to reach the per-class launches at small sizes)
  *   "h16_segcap" (tests) caps the fp16 projection's per-workgroup fix-up segment.
- *   "wide_image"       1 (default) = keep the fp16 row image for d > 64 too (d % 8 == 0): the
- *                      wide projection reads it (k_project_h16_wide); 0 = the f32 rows */
+ *   "wide_image"       1 = keep the fp16 row image for d > 64 too (d % 8 == 0): the wide
+ *                      projection reads it (k_project_h16_wide); 0 (default) = the f32 rows
+ *   "long_runs"        1 (default) = runs over 896 rows at d = 16 / 32 through k_merge_long
+ *                      (Gram bit matrix + one walk step per merge); 0 = k_merge_huge */
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
 /* Any option above, plus read-only diagnostics: "fp16_image" (1 = the loaded rows have the fp16
  * image), "last_hash_kernel" (klsh_hash_keys' projection kernel: 0 packed chains, 1 fp16-image

@@ -182,7 +182,7 @@ struct klsh_ctx {
   // option "projection" asks for the exact packed chains; every row store of the merge kernels
   // writes it too (store_row4 / store_row1)
   uint16_t* xh_alloc = nullptr;
-  bool wide_image = true;  // option "wide_image": the image for d > 64 too (k_project_h16_wide)
+  bool wide_image = false;  // option "wide_image": the image for d > 64 too (k_project_h16_wide)
   bool shadow_wanted(int d_) const {
     return pw.variant != klsh::kProjPacked && klsh::shadow_width_ok(d_) && (d_ <= 64 || wide_image);
   }
@@ -1771,6 +1771,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->pw.variant = (uint32_t)value;
     return ctx->apply_projection_variant();
   }
+  if (n == "long_runs") {  // (2, 3: diagnostics variants)
+    if (value < 0 || value > 4) return fail(KLSH_E_ARG, "long_runs must be 0, 1 or 4");
+    ctx->mw.long_off = value == 1 ? 0u : value == 0 ? 1u : (uint32_t)value;
+    return 0;
+  }
   if (n == "wide_image") {
     if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_image must be 0 or 1");
     KLSH_HIP(hipSetDevice(ctx->device));
@@ -1830,6 +1835,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "tail_merge_rows") *value = klsh::tail_merge_max(ctx->mw);
   else if (n == "small_screen") *value = ctx->mw.small_screen;
   else if (n == "wide_image") *value = ctx->wide_image;
+  else if (n == "long_runs") *value = ctx->mw.long_off ? 0 : 1;
   else if (n == "fp16_image") *value = ctx->rows.xh != nullptr;
   else if (n == "last_hash_kernel") *value = ctx->last_hash_kernel;
   else if (n == "last_hash_close_pairs") *value = (int64_t)ctx->last_hash_close;

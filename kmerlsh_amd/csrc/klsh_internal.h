@@ -152,6 +152,7 @@ struct MergeWork {
   // kLongRows / 64 words, and the number of workgroups it has room for (0: k_merge_huge)
   uint64_t* long_P;
   uint32_t long_groups;
+  uint32_t long_off;  // option "long_runs" = 0: k_merge_huge for them instead
   // launch sizes (klsh_set_option; 0 = the measured default, see the launch code)
   uint32_t small_grid;       // "small_grid": the small-run merge's persistent launch
   uint32_t tail_nbig;        // "tail_big_groups": k_merge_tail's big-run workgroups

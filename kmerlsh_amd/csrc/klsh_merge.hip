@@ -2626,6 +2626,9 @@ __device__ __forceinline__ void long_run(uint32_t p, uint32_t b, uint64_t* __res
         cnt[rp] = 0u;
         hd[cp] = hdp;
       }
+      // the previous step's new row to memory (wave 0's copy): not during that step, when other
+      // waves were still reading the old row for their own consensus
+      if (wv == 0 && lane < (uint32_t)D) store_row1(r, (size_t)slot[cp] * dp + lane, cwall[0][lane]);
       wave_lds_fence();
     }
     if (best == kNone64) break;
@@ -2650,10 +2653,11 @@ __device__ __forceinline__ void long_run(uint32_t p, uint32_t b, uint64_t* __res
     // consensus (funcAB.cc:65), current row first, into this wave's copy of the new row c
     const float fa = (float)(int)ca, fbc = (float)(int)cb, fn = (float)(int)(ca + cb);
     if (lane < (uint32_t)D) {
-      const float v = consensus(ld_l2(r.x + (size_t)s_r * dp + lane), fa,
-                                ld_l2(r.x + (size_t)s_c * dp + lane), fbc, fn);
+      // row c as of now: the previous step's new row if it is that row again (its store above may
+      // not have landed), else memory (every earlier store landed at its step's barrier)
+      const float xc = have && c == cp ? cwall[wv][lane] : ld_l2(r.x + (size_t)s_c * dp + lane);
+      const float v = consensus(ld_l2(r.x + (size_t)s_r * dp + lane), fa, xc, fbc, fn);
       cwall[wv][lane] = v;
-      if (wv == 0) store_row1(r, (size_t)s_c * dp + lane, v);
     }
     if (t == 0) r.nxt[tr] = hc;  // ids_current ++ ids_candidate (funcAB.cc:51-55)
     wave_lds_fence();
@@ -2723,7 +2727,7 @@ __device__ __forceinline__ void long_run(uint32_t p, uint32_t b, uint64_t* __res
           d4[2] = d4[2] + xr[kp][k + 2] * u.z;
           d4[3] = d4[3] + xr[kp][k + 3] * u.w;
         }
-        uint32_t v = prescreen(dc, (d4[0] + d4[1]) + (d4[2] + d4[3]), sy * sc_a);
+        uint32_t v = w.long_off == 3u ? 2u : prescreen(dc, (d4[0] + d4[1]) + (d4[2] + d4[3]), sy * sc_a);
         if (v == 2u) {  // rare: the reference's sequential chains (distance.cc:27-38)
           float nn = 0.0f, dot = 0.0f;
 #pragma unroll
@@ -2808,30 +2812,49 @@ __device__ __forceinline__ void long_run(uint32_t p, uint32_t b, uint64_t* __res
 #endif
 }
 
+// One index space over the >896-row list and (list2, option long_runs = 4) the 385..896-row
+// list after it: the longest walks first.
 template <int D>
 __global__ __launch_bounds__(kLongNT) void k_merge_long(const uint2* __restrict__ list,
                                                         const uint32_t* count_ptr,
+                                                        const uint2* __restrict__ list2,
+                                                        const uint32_t* count2_ptr,
                                                         uint32_t* __restrict__ slots, Decider dc,
                                                         Rows r, MergeWork w, Counters* ctr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   kt_begin(w.kt, KC_HUGE);
   const uint32_t count = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t count2 =
+      list2 ? __hip_atomic_load(count2_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   uint64_t* P = w.long_P + (size_t)blockIdx.x * kLongRows * kLongWords;
-  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {  // block-uniform
-    const uint2 e = list[li];
-    if (e.y <= kLongRows) long_run<D>(e.x, e.y, P, slots, dc, r, w, ctr, smem);
-    else huge_runs<D, kLongNT>(list, li + 1u, li, 1u << 30, slots, dc, r, w, ctr, smem);
+  for (uint32_t li = blockIdx.x; li < count + count2; li += gridDim.x) {  // block-uniform
+    const uint2* l = li < count ? list : list2;
+    const uint32_t k = li < count ? li : li - count;
+    const uint2 e = l[k];
+    const uint32_t cap = w.long_off == 2u ? (uint32_t)LongRegs<D>::KP * kLongNT : kLongRows;
+    if (e.y <= cap) long_run<D>(e.x, e.y, P, slots, dc, r, w, ctr, smem);
+    else huge_runs<D, kLongNT>(l, k + 1u, k, 1u << 30, slots, dc, r, w, ctr, smem);
     __syncthreads();
   }
   kt_end(w.kt, KC_HUGE);
 }
 
+// k_merge_long takes the >896-row runs (and with option long_runs = 4 the 385..896-row ones)
+static bool long_ok_for(const MergeWork& w, const Decider& dc, const Rows& r) {
+  return w.long_P && w.long_groups && w.long_off != 1u && dc.fast && (r.d == 16 || r.d == 32);
+}
+static bool long896(const MergeWork& w, const Decider& dc, const Rows& r) {
+  return w.long_off == 4u && long_ok_for(w, dc, r);
+}
+
 static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, const Rows& r,
                         Counters* ctr, uint32_t n, hipStream_t s) {
-  if (w.huge_fold) return;  // the 385..896-row kernel walks them (k_merge_big)
+  const bool with896 = long896(w, dc, r);
+  if (w.huge_fold && !with896) return;  // the 385..896-row kernel walks them (k_merge_big)
   uint32_t g = (uint32_t)std::min<uint64_t>(512, n / (kBigRows[kBigClasses - 1] + 1) + 1);
-  if (w.huge_cap) g = std::min(g, w.huge_cap);  // (the kernel strides over its list)
-  if (w.long_P && w.long_groups && dc.fast && (r.d == 16 || r.d == 32)) {
+  if (w.huge_cap && !with896) g = std::min(g, w.huge_cap);  // (the kernel strides over its list)
+  if (with896) g = (uint32_t)std::min<uint64_t>(1024, n / (kBigRows[kBigClasses - 2] + 1) + 1);
+  if (long_ok_for(w, dc, r)) {
     const size_t lds = std::max(long_lds(), huge_lds(r.d, r.dp, kLongNT));
     static const bool lds_ok = [lds] {
       bool ok = true;
@@ -2843,10 +2866,12 @@ static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, 
     }();
     (void)lds_ok;
     g = std::min(g, w.long_groups);
+    const uint2* l2 = with896 ? w.big[kBigClasses - 1] : nullptr;
+    const uint32_t* c2 = &w.rc->n_big[kBigClasses - 1].v;
     if (r.d == 16)
-      k_merge_long<16><<<g, kLongNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr);
+      k_merge_long<16><<<g, kLongNT, lds, s>>>(w.huge, &w.rc->n_huge.v, l2, c2, slots, dc, r, w, ctr);
     else
-      k_merge_long<32><<<g, kLongNT, lds, s>>>(w.huge, &w.rc->n_huge.v, slots, dc, r, w, ctr);
+      k_merge_long<32><<<g, kLongNT, lds, s>>>(w.huge, &w.rc->n_huge.v, l2, c2, slots, dc, r, w, ctr);
     return;
   }
   const size_t lds = huge_lds(r.d, r.dp, kHugeNT);
@@ -3347,7 +3372,8 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   // in front of the >896-row runs on the main stream — serialised, the two long-walk classes
   // make the main stream the critical path (C4 1794 -> 1432 ms); with a handful of them (C2)
   // the main stream is the better place (measured 281-285 vs 284-294 ms)
-  launch_big<D, 896, 256, false>(w, 3, slots, dc, r, ctr, n, w.big896_aux ? f.lane(2) : s);
+  if (!long896(w, dc, r))
+    launch_big<D, 896, 256, false>(w, 3, slots, dc, r, ctr, n, w.big896_aux ? f.lane(2) : s);
   launch_huge(w, slots, dc, r, ctr, n, s);
   // 129..192 rows: two workgroups per CU (62 KB of LDS at d = 64, VGPRs capped at 256 like the
   // 65..128 class), ahead of 65..128 on aux 1

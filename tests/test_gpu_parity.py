@@ -141,7 +141,7 @@ def adversarial_rows(rng, n, d, w):
 
 @pytest.mark.parametrize("d,h,wide_image", [(64, 23, 1), (32, 18, 1), (16, 9, 1), (64, 31, 1),
                                             (32, 1, 1), (8, 7, 1), (512, 20, 1), (512, 20, 0),
-                                            (100, 31, 1), (72, 5, 1), (72, 5, 0), (136, 32, 1)])
+                                            (100, 31, 1), (72, 5, 1), (72, 5, 0), (136, 31, 1)])
 def test_hash_keys_close_calls_vs_oracle(engine, oracle, d, h, wide_image):
     """The loop's projection kernels (klsh_hash_keys uses the same dispatch and the fp16 row image
     at d = 16/32/64 and at d > 64 with d % 8 == 0: k_project_h16_wide; wide_image = 0 or
@@ -417,6 +417,21 @@ def test_long_runs_vs_oracle(engine, oracle, b, d, groups, noise, thr):
     assert_same_result(got, *oracle.pcluster(rows, thr))
 
 
+@pytest.mark.parametrize("b,d,groups,noise,thr", [
+    (385, 32, 30, 0.05, 0.95), (700, 16, 50, 0.1, 0.8), (896, 32, 200, 0.05, 0.95),
+    (640, 32, 640, 0.3, 0.99), (500, 32, 3, 0.02, 0.9)])
+def test_long_runs_385_896_vs_oracle(engine, oracle, b, d, groups, noise, thr):
+    """Option long_runs = 4: the 385..896-row runs through k_merge_long too (after the longer
+    ones, in the same launch)."""
+    rng = np.random.default_rng(b * 13 + d)
+    rows = clustered(rng, b, d, groups, noise)
+    with options(engine, tail_merge_rows=1, long_runs=4):
+        engine.load_rows(rows)
+        engine.pcluster(thr)
+        got = engine.result()
+    assert_same_result(got, *oracle.pcluster(rows, thr))
+
+
 @pytest.mark.parametrize("special", ["nan", "zero", "huge", "tiny"])
 def test_long_runs_special_rows(engine, oracle, special):
     """A long run with a row the pre-screen cannot call (NaN, zero, 1e30, 1e-30 scale): the
@@ -437,6 +452,23 @@ def test_long_runs_special_rows(engine, oracle, special):
         engine.pcluster(0.9)
         got = engine.result()
     assert_same_result(got, *oracle.pcluster(rows, 0.9))
+
+
+@pytest.mark.parametrize("n,groups,noise", [(200000, 100, 0.03), (300000, 120, 0.3)])
+def test_long_runs_many_at_once_vs_oracle(engine, oracle, n, groups, noise):
+    """Hundreds of runs over 896 rows in every launch of k_merge_long (one workgroup each, up
+    to 256 at once), repeated: the same trace, counter and result as the oracle every time."""
+    rng = np.random.default_rng(n + groups)
+    rows = clustered(rng, n, 32, groups, noise)
+    want = oracle.cluster(rows, 0.8, 3, 1000000, 17, 4)
+    for _ in range(3):
+        with options(engine, tail_merge_rows=1):
+            engine.load_rows(rows)
+            trace, counter, st = engine.cluster(0.8, 3, 1000000, 17, 4)
+            got = engine.result()
+        assert st["kern"]["huge"]["launches"] > 0
+        assert np.array_equal(trace, want[3]) and counter == want[4]
+        assert_same_result(got, *want[:3])
 
 
 def test_long_runs_in_the_loop_vs_oracle(engine, oracle):
