@@ -502,7 +502,8 @@ def main():
     # link, the removed row's count) — merges counted over the whole iteration (~97 % of them are
     # small-run merges on C2).  The bench line's "roofline" is the one with the larger time per step.
     roofline = kernel_rooflines(args.config, stats, args.steps, d, trace,
-                                bool(eng.get_option("fp16_image")))
+                                bool(eng.get_option("fp16_image")) and
+                                (d <= 64 or bool(eng.get_option("wide_projection"))))
     # the whole loop against HBM, SURVEY.md §8(d): B_t = N_t (8d + 16) + M_t (4d + 8) bytes per
     # iteration (rows read by the projection and by the merge, keys and order written and read;
     # per merge the new row and a member link), summed over the timed steps

@@ -216,6 +216,13 @@ struct klsh_ctx {
   // schedule (0 = all).  Prefix parity tests of the long configs use it; results of the
   // iterations that do run are unchanged.
   int stop_after = 0;
+  int progress = 0;  // option "progress": a line on stderr every this many iterations (profiling runs)
+  void tick(int it) const {
+    if (progress > 0 && it % progress == 0) {
+      fprintf(stderr, "[klsh] iteration %d\n", it);
+      fflush(stderr);
+    }
+  }
   // "hyperplane_window" (klsh_set_option): rows drawn up front per call (0 = the default bound)
   uint64_t hyperplane_window = 0;
 
@@ -1149,6 +1156,7 @@ static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, 
       const int h = floor_log2(n_in);
       if (nt_trace) nt_trace[ch.it0 + c] = n_in;
       st->iterations += 1;
+      ctx->tick(ch.it0 + c);
       st->project_launches += 1;  // (no HIP events around queued launches: not in project_ms)
       *rng_counter += (uint64_t)h;
       st->hyperplanes += (uint64_t)h;
@@ -1214,6 +1222,7 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     const double t_it = iter_log ? now_ms() : 0.0;
     if (nt_trace) nt_trace[it] = n;
     st->iterations += 1;
+    ctx->tick(it);
     if (n == 0) {  // the reference aborts here (cluster.cc:194 on an empty vector); no-op
       threshold -= sim_step;
       continue;
@@ -1425,6 +1434,7 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
     }
     if (nt_trace) nt_trace[it] = N;
     st->iterations += 1;
+    ctx->tick(it);
     if (N == 0) {
       threshold -= sim_step;
       continue;
@@ -1759,6 +1769,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->hyperplane_window = (uint64_t)value;
     return 0;
   }
+  if (n == "progress") {
+    if (value < 0 || value > INT32_MAX) return fail(KLSH_E_ARG, "progress must be >= 0");
+    ctx->progress = (int)value;
+    return 0;
+  }
   if (n == "stop_after") {
     if (value < 0 || value > INT32_MAX) return fail(KLSH_E_ARG, "stop_after must be in [0, 2^31)");
     ctx->stop_after = (int)value;
@@ -1770,6 +1785,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     KLSH_HIP(hipSetDevice(ctx->device));
     ctx->pw.variant = (uint32_t)value;
     return ctx->apply_projection_variant();
+  }
+  if (n == "wide_projection") {
+    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_projection must be 0 or 1");
+    ctx->pw.wide_h16 = (uint32_t)value;
+    return 0;
   }
   if (n == "long_runs") {  // (2, 3: diagnostics variants)
     if (value < 0 || value > 4) return fail(KLSH_E_ARG, "long_runs must be 0, 1 or 4");
@@ -1821,6 +1841,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "tail_local") *value = ctx->tail_local;
   else if (n == "hyperplane_window") *value = (int64_t)ctx->hyperplane_window;
   else if (n == "stop_after") *value = ctx->stop_after;
+  else if (n == "progress") *value = ctx->progress;
   else if (n == "projection") *value = ctx->pw.variant;
   else if (n == "comm_timeout_s") *value = (int64_t)ctx->comm_timeout_s;
   else if (n == "h16_grid") *value = ctx->pw.h16_grid;
@@ -1835,7 +1856,8 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "tail_merge_rows") *value = klsh::tail_merge_max(ctx->mw);
   else if (n == "small_screen") *value = ctx->mw.small_screen;
   else if (n == "wide_image") *value = ctx->wide_image;
-  else if (n == "long_runs") *value = ctx->mw.long_off ? 0 : 1;
+  else if (n == "long_runs") *value = ctx->mw.long_off == 1u ? 0 : ctx->mw.long_off == 0u ? 1 : ctx->mw.long_off;
+  else if (n == "wide_projection") *value = ctx->pw.wide_h16;
   else if (n == "fp16_image") *value = ctx->rows.xh != nullptr;
   else if (n == "last_hash_kernel") *value = ctx->last_hash_kernel;
   else if (n == "last_hash_close_pairs") *value = (int64_t)ctx->last_hash_close;

@@ -152,7 +152,9 @@ struct MergeWork {
   // kLongRows / 64 words, and the number of workgroups it has room for (0: k_merge_huge)
   uint64_t* long_P;
   uint32_t long_groups;
-  uint32_t long_off;  // option "long_runs" = 0: k_merge_huge for them instead
+  // option "long_runs": 4 (default) = k_merge_long also takes the 385..896-row runs, 1 = only
+  // the longer ones, 0 = k_merge_huge for those (long_off = 1)
+  uint32_t long_off = 4;
   // launch sizes (klsh_set_option; 0 = the measured default, see the launch code)
   uint32_t small_grid;       // "small_grid": the small-run merge's persistent launch
   uint32_t tail_nbig;        // "tail_big_groups": k_merge_tail's big-run workgroups
@@ -230,6 +232,7 @@ struct ProjectWork {
   uint32_t fix_grid;   // "fix_grid": wide-row fix-up workgroups
   uint32_t segcap;     // "h16_segcap" (tests): fix-up entries per fp16-projection workgroup
   uint32_t variant;    // "projection": kProjAuto / kProjPacked / kProjScreen (set per launch)
+  uint32_t wide_h16;   // "wide_projection": 1 = wide rows projected from the fp16 image
 };
 // Projection variants (klsh_set_option "projection"): the default picks the certified
 // matrix-core screen where it exists (the fp16 row image at d = 16 / 32 / 64, bf16x3 above 64)

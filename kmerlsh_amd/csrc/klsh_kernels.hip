@@ -956,7 +956,7 @@ int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_
       // stamped as one span: the screen (start) and the fix-up of its close calls (end)
       KTime k1 = kt;
       k1.fold = -1;
-      if (r.xh)  // the fp16 image (kept for d > 64 too unless option wide_image = 0)
+      if (r.xh && pw->wide_h16)  // the fp16 image (option wide_projection; kept: wide_image)
         k_project_h16_wide<<<gm, dim3(kWideNT), lds, s>>>(r.xh, r.d, r.dp, slots, keys, n, r.x, W,
                                                           h, key_or, h16_eps(r.d), h16_abs(r.d),
                                                           *pw, kt);
@@ -966,7 +966,7 @@ int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_
                                                            *pw, kt);
       const uint32_t fcap = pw->fix_grid ? std::max(16u, pw->fix_grid) : 1024u;  // "fix_grid"
       k_project_fix<<<fcap, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
-      return r.xh ? kPkWideH16 : kPkWide;
+      return r.xh && pw->wide_h16 ? kPkWideH16 : kPkWide;
     }
   }
   if (h16_ok(r, pw) && h > 0) {

@@ -153,7 +153,7 @@ def test_hash_keys_close_calls_vs_oracle(engine, oracle, d, h, wide_image):
     rng = np.random.default_rng(11 + d + h)
     w, _ = _native.hyperplanes(7 + d, 0, h, d)
     rows = adversarial_rows(rng, 4000, d, w)
-    with options(engine, wide_image=wide_image):
+    with options(engine, wide_image=wide_image, wide_projection=wide_image):
         got = engine.hash_keys(rows, w)
         kern = engine.get_option("last_hash_kernel")
     assert np.array_equal(got, oracle.keys(rows, w)), (d, h)
@@ -482,6 +482,28 @@ def test_long_runs_in_the_loop_vs_oracle(engine, oracle):
         trace, counter, st = engine.cluster(0.8, 6, 1000000, 41, 4)
         got = engine.result()
     assert st["kern"]["huge"]["launches"] > 0
+    assert np.array_equal(trace, want[3]) and counter == want[4]
+    assert_same_result(got, *want[:3])
+
+
+@pytest.mark.parametrize("d,screen", [(512, 1), (136, 1), (512, 0)])
+def test_wide_small_screen_vs_oracle(engine, oracle, d, screen):
+    """Wide rows with the fp16 image kept (option wide_image): the small runs screened on it
+    first (k_small_screen_wide, one launch per class), only the runs it cannot rule out merged on
+    the f32 rows — same trace, counter and result bits as the oracle, with rows the image cannot
+    carry (fp16 overflow, all-zero image of a nonzero row, zero, NaN)."""
+    rng = np.random.default_rng(d + 3)
+    rows = clustered(rng, 40000, d, 1500, 0.05)
+    rows[5] *= np.float32(1e5)
+    rows[11] *= np.float32(1e-9)
+    rows[13] = 0.0
+    rows[17, 2] = np.nan
+    want = oracle.cluster(rows, 0.8, 5, 1000000, 21, 4)
+    with options(engine, wide_image=1, small_screen=screen, tail_merge_rows=1):
+        engine.load_rows(rows)
+        trace, counter, st = engine.cluster(0.8, 5, 1000000, 21, 4)
+        got = engine.result()
+    assert (st["kern"]["screen"]["launches"] > 0) == bool(screen)
     assert np.array_equal(trace, want[3]) and counter == want[4]
     assert_same_result(got, *want[:3])
 

@@ -1,8 +1,9 @@
 #!/bin/bash
 # Round profiles on the GPU box (run through gpurun from the repo root):
-#   C2 bench line, rocprofv3 kernel stats of one C2 step, FETCH_SIZE / WRITE_SIZE of the projection
-#   and of the small-run merge (separate --pmc passes), kernel stats of C4 and C5.  Outputs under gpurun_out/prof/.
-#   tools/collect_profiles.sh [c2|all]
+#   C2 bench line, rocprofv3 kernel stats of one C2 step, FETCH_SIZE / WRITE_SIZE of the projection,
+#   the small-run screen and the small-run merge (separate --pmc passes, the engine printing a
+#   progress line every 25 iterations), kernel stats of C4 and C5.  Outputs under gpurun_out/prof/.
+#   tools/collect_profiles.sh [c2|pmc|all]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 out=gpurun_out/prof
@@ -16,12 +17,17 @@ run() {  # name seconds cmd...
   echo "=== $name rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 }
-run c2_bench 300 python bench.py --steps 3 --warmup 1
-run c2_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c2_stats -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline none
-for k in k_project k_merge_small; do
-  run c2_fetch_$k 300 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex $k -d $out/c2_fetch_$k -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline none
-  run c2_write_$k 300 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex $k -d $out/c2_write_$k -o run -- python bench.py --steps 1 --warmup 0 --cpu-baseline none
-done
+B="python bench.py --steps 1 --warmup 0 --cpu-baseline none --option progress=25"
+if [ "$1" != pmc ]; then
+  run c2_bench 300 python bench.py --steps 3 --warmup 1
+  run c2_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c2_stats -o run -- $B
+fi
+if [ "$1" = pmc ] || [ "$1" = all ]; then
+  for k in k_project k_small_screen k_merge_small; do
+    run c2_fetch_$k 400 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex $k -d $out/c2_fetch_$k -o run -- $B
+    run c2_write_$k 400 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex $k -d $out/c2_write_$k -o run -- $B
+  done
+fi
 if [ "$1" = all ]; then
   run c4_bench 400 python bench.py --config c4 --steps 2 --warmup 1 --cpu-baseline none
   run c5_bench 400 python bench.py --config c5 --steps 2 --warmup 1 --cpu-baseline none
