@@ -33,10 +33,17 @@ struct RcclComm final : Comm {
     nc = nullptr;
   }
   int wait(hipStream_t s) override {
+    return poll([&] { return hipStreamQuery(s); });
+  }
+  int wait_event(hipEvent_t e) override {
+    return poll([&] { return hipEventQuery(e); });
+  }
+  template <class Query>
+  int poll(Query query) {
     if (aborted) return check(ncclSuccess, "wait");
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t polls = 0;; ++polls) {
-      const hipError_t q = hipStreamQuery(s);
+      const hipError_t q = query();
       if (q == hipSuccess) return 0;
       if (q != hipErrorNotReady) {
         err = std::string("stream: ") + hipGetErrorString(q);

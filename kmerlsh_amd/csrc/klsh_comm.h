@@ -57,6 +57,14 @@ struct Comm {
     }
     return 0;
   }
+  // Wait for event e, recorded on a stream that may hold this group's collectives (as wait()).
+  virtual int wait_event(hipEvent_t e) {
+    if (hipEventSynchronize(e) != hipSuccess) {
+      err = "event sync";
+      return -1;
+    }
+    return 0;
+  }
   double timeout_s = 600.0;  // option "comm_timeout_s"
   bool aborted = false;
   std::string err;

@@ -216,6 +216,7 @@ struct klsh_ctx {
   // schedule (0 = all).  Prefix parity tests of the long configs use it; results of the
   // iterations that do run are unchanged.
   int stop_after = 0;
+  hipEvent_t counts_ev = nullptr;  // sharded loop: the send counts are on the host
   int progress = 0;  // option "progress": a line on stderr every this many iterations (profiling runs)
   void tick(int it) const {
     if (progress > 0 && it % progress == 0) {
@@ -319,6 +320,8 @@ struct klsh_ctx {
       if (e) (void)hipEventDestroy(e), e = nullptr;
     for (auto& e : sev)
       if (e) (void)hipEventDestroy(e), e = nullptr;
+    if (counts_ev) (void)hipEventDestroy(counts_ev);
+    counts_ev = nullptr;
     for (int i = 0; i < klsh::kMergeStreams; ++i) {
       if (mw.join[i]) (void)hipEventDestroy(mw.join[i]);
       if (mw.aux[i]) (void)hipStreamDestroy(mw.aux[i]);
@@ -460,7 +463,9 @@ struct klsh_ctx {
     if (same_stream && k0 >= w_k0 && k0 + count <= w_k0 + w_count) return 0;
     const double t0 = now_ms();
     if (!(same_stream && k0 >= w_k0 && k0 + count <= w_k0 + w_cap)) {
-      const uint64_t cap = std::max<uint64_t>({count, 4096, w_cap});
+      // (the window's row capacity carries over only for the same row width: w_cap rows of
+      // another dp would scale the allocation by the width ratio on every change of d)
+      const uint64_t cap = std::max<uint64_t>({count, 4096, same_stream ? w_cap : 0});
       if (!W || cap * (uint64_t)dp > w_alloc) {
         dfree(W);
         if (int e = dalloc(&W, cap * (uint64_t)dp)) return e;
@@ -1461,7 +1466,15 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
       return comm_fail("bin histogram allgather");
     klsh::launch_bin_split(ctx->bins_all, W, nbins, N, ctx->owner, ctx->cntmat, s);
     KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->cntmat, 4ull * W * W, hipMemcpyDeviceToHost, s));
-    if (timed_comm([&] { return cm->wait(s); })) return comm_fail("send counts");
+    if (!ctx->counts_ev) KLSH_HIP(hipEventCreateWithFlags(&ctx->counts_ev, hipEventDisableTiming));
+    KLSH_HIP(hipEventRecord(ctx->counts_ev, s));
+    // 2a. the stable partition by owner needs only the device's ownership map: it is queued
+    //     before the host waits (for the counts only, not for it), so it runs during the round trip
+    if (klsh::launch_partition(ctx->keys, ctx->order, n_g, shift, ctx->owner, W, ctx->nk1,
+                               ctx->tile_sums, ctx->ctr, ctx->sbuf, s))
+      return fail(KLSH_E_ARG, "partition: unsupported world size");
+    KLSH_HIP(hipGetLastError());
+    if (timed_comm([&] { return cm->wait_event(ctx->counts_ev); })) return comm_fail("send counts");
     uint32_t m_g = 0;
     for (int r = 0; r < W; ++r) {
       scnt[r] = 8ull * ctx->h_small[g * W + r];
@@ -1471,11 +1484,7 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
       m_g += ctx->h_small[r * W + g];
     }
 
-    // 2. exchange (key, slot) pairs: stable partition by owner, all-to-all-v
-    if (klsh::launch_partition(ctx->keys, ctx->order, n_g, shift, ctx->owner, W, ctx->nk1,
-                               ctx->tile_sums, ctx->ctr, ctx->sbuf, s))
-      return fail(KLSH_E_ARG, "partition: unsupported world size");
-    KLSH_HIP(hipGetLastError());
+    // 2b. exchange the partitioned (key, slot) pairs: all-to-all-v
     if (timed_comm([&] {
           return cm->alltoallv(ctx->sbuf, scnt.data(), soff.data(), ctx->rbuf, rcnt.data(),
                                roff.data(), s);
