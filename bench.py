@@ -338,7 +338,8 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
         if c == "huge" and d in (16, 32):
             name = f"k_merge_long<{d}>"
         pmc = pmc_traffic(config, c) or pmc_traffic(config, {"project": "k_project",
-                                                             "small": "k_merge_small"}.get(c, ""))
+                                                             "small": "k_merge_small",
+                                                             "screen": "k_small_screen"}.get(c, ""))
         e = {"kernel": name, "class": c, "bound": "hbm", "achieved": round(ach, 2),
              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
              "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,

@@ -3,7 +3,7 @@
 #   C2 bench line, rocprofv3 kernel stats of one C2 step, FETCH_SIZE / WRITE_SIZE of the projection,
 #   the small-run screen and the small-run merge (separate --pmc passes, the engine printing a
 #   progress line every 25 iterations), kernel stats of C4 and C5.  Outputs under gpurun_out/prof/.
-#   tools/collect_profiles.sh [c2|pmc|all]
+#   tools/collect_profiles.sh [c2|pmc|c45|all]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 out=gpurun_out/prof
@@ -18,7 +18,7 @@ run() {  # name seconds cmd...
   [ $rc -eq 0 ] || exit $rc
 }
 B="python bench.py --steps 1 --warmup 0 --cpu-baseline none --option progress=25"
-if [ "$1" != pmc ]; then
+if [ "$1" != pmc ] && [ "$1" != c45 ]; then
   run c2_bench 300 python bench.py --steps 3 --warmup 1
   run c2_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c2_stats -o run -- $B
 fi
@@ -28,7 +28,7 @@ if [ "$1" = pmc ] || [ "$1" = all ]; then
     run c2_write_$k 400 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex $k -d $out/c2_write_$k -o run -- $B
   done
 fi
-if [ "$1" = all ]; then
+if [ "$1" = all ] || [ "$1" = c45 ]; then
   run c4_bench 400 python bench.py --config c4 --steps 2 --warmup 1 --cpu-baseline none
   run c5_bench 400 python bench.py --config c5 --steps 2 --warmup 1 --cpu-baseline none
   run c4_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c4_stats -o run -- python bench.py --config c4 --steps 1 --warmup 0 --cpu-baseline none

@@ -42,7 +42,7 @@ for cfg in ("c2", "c4", "c5"):
 summary = {}
 # (kernel key, regex used by collect_profiles.sh, launches to keep: the main loop's — the init
 # pass's launch comes first)
-for key, keep in (("k_project", 500), ("k_merge_small", None)):
+for key, keep in (("k_project", 500), ("k_merge_small", None), ("k_small_screen", None)):
     vals = {}
     for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         p = one(f"c2_{kind}_{key}/**/run_counter_collection.csv") or (
