@@ -689,8 +689,6 @@ klsh_ctx* klsh_create(int device, int* err) {
   for (int i = 0; i < klsh::kMergeStreams; ++i) {
 #ifdef KLSH_AUX1_HI  // A/B: the 65..192-row stream at the high priority too
     const bool hi = i <= 1;
-#elif defined(KLSH_AUX2_HI)  // A/B: the small-run stream (screen + merge) at the high priority
-    const bool hi = i == 0 || i == 2;
 #else
     const bool hi = i == 0;
 #endif

@@ -1154,7 +1154,10 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ vout,
                                                     const uint32_t* __restrict__ dtot, int lb,
                                                     int bucket_thr, MergeWork w) {
-  constexpr uint32_t kChunk = 4096, kItems = 16;
+#ifndef KLSH_TL_ITEMS
+#define KLSH_TL_ITEMS 16
+#endif
+  constexpr uint32_t kItems = KLSH_TL_ITEMS, kWave = kItems * 64u, kChunk = 4u * kWave;
   __shared__ uint32_t cnt[1024];      // low-digit counts, then their exclusive starts
   __shared__ uint32_t run_[1024];     // running count of each digit over the rounds
   __shared__ uint32_t wc[4][1024];    // per-wave digit counts of a round, then wave prefixes
@@ -1258,13 +1261,13 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     uint32_t k[kItems], v[kItems], lr[kItems];
 #pragma unroll
     for (int j = 0; j < (int)kItems; ++j) {
-      const uint32_t p = r0 + wv * 1024u + (uint32_t)j * 64u + lane;
+      const uint32_t p = r0 + wv * kWave + (uint32_t)j * 64u + lane;
       k[j] = p < m ? kin[base + p] : 0u;
       v[j] = p < m ? vin[base + p] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < (int)kItems; ++j) {
-      const bool valid = r0 + wv * 1024u + (uint32_t)j * 64u + lane < m;
+      const bool valid = r0 + wv * kWave + (uint32_t)j * 64u + lane < m;
       const uint32_t dig = k[j] & MASK;
       uint64_t match = __ballot(valid);
       for (int b = 0; b < lb; ++b) {
@@ -1291,7 +1294,7 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < (int)kItems; ++j) {
-      if (r0 + wv * 1024u + (uint32_t)j * 64u + lane < m) {
+      if (r0 + wv * kWave + (uint32_t)j * 64u + lane < m) {
         const uint32_t o = base + wc[wv][k[j] & MASK] + lr[j];
         kout[o] = k[j];
         vout[o] = v[j];
