@@ -180,8 +180,11 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *   "h16_segcap" (tests) caps the fp16 projection's per-workgroup fix-up segment.
  *   "wide_image"       1 = keep the fp16 row image for d > 64 too (d % 8 == 0): the wide
  *                      projection reads it (k_project_h16_wide); 0 (default) = the f32 rows
- *   "long_runs"        1 (default) = runs over 896 rows at d = 16 / 32 through k_merge_long
- *                      (Gram bit matrix + one walk step per merge); 0 = k_merge_huge */
+ *   "long_runs"        4 (default) = runs over 384 rows at d = 16 / 32 through k_merge_long
+ *                      (Gram bit matrix + one walk step per merge); 1 = only runs over 896 rows;
+ *                      0 = k_merge_huge for those
+ *   "wide_projection"  1 = wide rows projected from the fp16 image (needs wide_image = 1)
+ *   "progress"         N > 0: a line on stderr every N iterations (long profiling runs) */
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
 /* Any option above, plus read-only diagnostics: "fp16_image" (1 = the loaded rows have the fp16
  * image), "last_hash_kernel" (klsh_hash_keys' projection kernel: 0 packed chains, 1 fp16-image

@@ -1800,9 +1800,9 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->pw.wide_h16 = (uint32_t)value;
     return 0;
   }
-  if (n == "long_runs") {  // (2, 3: diagnostics variants)
-    if (value < 0 || value > 4) return fail(KLSH_E_ARG, "long_runs must be 0, 1 or 4");
-    ctx->mw.long_off = value == 1 ? 0u : value == 0 ? 1u : (uint32_t)value;
+  if (n == "long_runs") {
+    if (value != 0 && value != 1 && value != 4) return fail(KLSH_E_ARG, "long_runs must be 0, 1 or 4");
+    ctx->mw.long_off = value == 1 ? 0u : value == 0 ? 1u : 4u;
     return 0;
   }
   if (n == "wide_image") {

@@ -2730,7 +2730,7 @@ __device__ __forceinline__ void long_run(uint32_t p, uint32_t b, uint64_t* __res
           d4[2] = d4[2] + xr[kp][k + 2] * u.z;
           d4[3] = d4[3] + xr[kp][k + 3] * u.w;
         }
-        uint32_t v = w.long_off == 3u ? 2u : prescreen(dc, (d4[0] + d4[1]) + (d4[2] + d4[3]), sy * sc_a);
+        uint32_t v = prescreen(dc, (d4[0] + d4[1]) + (d4[2] + d4[3]), sy * sc_a);
         if (v == 2u) {  // rare: the reference's sequential chains (distance.cc:27-38)
           float nn = 0.0f, dot = 0.0f;
 #pragma unroll
@@ -2834,8 +2834,7 @@ __global__ __launch_bounds__(kLongNT) void k_merge_long(const uint2* __restrict_
     const uint2* l = li < count ? list : list2;
     const uint32_t k = li < count ? li : li - count;
     const uint2 e = l[k];
-    const uint32_t cap = w.long_off == 2u ? (uint32_t)LongRegs<D>::KP * kLongNT : kLongRows;
-    if (e.y <= cap) long_run<D>(e.x, e.y, P, slots, dc, r, w, ctr, smem);
+    if (e.y <= kLongRows) long_run<D>(e.x, e.y, P, slots, dc, r, w, ctr, smem);
     else huge_runs<D, kLongNT>(l, k + 1u, k, 1u << 30, slots, dc, r, w, ctr, smem);
     __syncthreads();
   }
