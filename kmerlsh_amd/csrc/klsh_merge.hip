@@ -3555,7 +3555,9 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   if (screen_ok(r, dc, w)) {
     float m0, a2;
     screen_margins(r.d, &m0, &a2);
-    const uint32_t sgrid = w.screen_grid ? std::max(64u, w.screen_grid) : 3072u;
+    // (option small_screen_grid; one-wave workgroups: 2048 → 207.9 / 207.8 vs 3072 → 211.2 /
+    // 211.1 ms per C2 step on one box, 1024 → 227–228, 1536 / 2560 within noise of 2048)
+    const uint32_t sgrid = w.screen_grid ? std::max(64u, w.screen_grid) : 2048u;
     k_small_screen<D><<<sgrid, 64, 0, f.lane(2)>>>(w, slots, r, dc.s_star, m0, a2, w.kt);
     MergeWork ws = w;
     ws.screened = 1u;
