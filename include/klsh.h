@@ -184,6 +184,9 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *                      (Gram bit matrix + one walk step per merge); 1 = only runs over 896 rows;
  *                      0 = k_merge_huge for those
  *   "wide_projection"  1 = wide rows projected from the fp16 image (needs wide_image = 1)
+ *   "wide_gram"        at d = 512 the group merges of runs of at least this many rows (8, 16, 32
+ *                      or 64; default 32) take their decisions from an MFMA Gram matrix with a
+ *                      certified margin, the uncertain pairs from the exact chains; 0 = none
  *   "progress"         N > 0: a line on stderr every N iterations (long profiling runs) */
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
 /* Any option above, plus read-only diagnostics: "fp16_image" (1 = the loaded rows have the fp16

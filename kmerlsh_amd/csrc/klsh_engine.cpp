@@ -1795,6 +1795,12 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->pw.variant = (uint32_t)value;
     return ctx->apply_projection_variant();
   }
+  if (n == "wide_gram") {
+    if (value != 0 && value != 8 && value != 16 && value != 32 && value != 64)
+      return fail(KLSH_E_ARG, "wide_gram must be 0, 8, 16, 32 or 64");
+    ctx->mw.wide_gram = (uint32_t)value;
+    return 0;
+  }
   if (n == "wide_projection") {
     if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_projection must be 0 or 1");
     ctx->pw.wide_h16 = (uint32_t)value;
@@ -1867,6 +1873,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "wide_image") *value = ctx->wide_image;
   else if (n == "long_runs") *value = ctx->mw.long_off == 1u ? 0 : ctx->mw.long_off == 0u ? 1 : ctx->mw.long_off;
   else if (n == "wide_projection") *value = ctx->pw.wide_h16;
+  else if (n == "wide_gram") *value = ctx->mw.wide_gram;
   else if (n == "fp16_image") *value = ctx->rows.xh != nullptr;
   else if (n == "last_hash_kernel") *value = ctx->last_hash_kernel;
   else if (n == "last_hash_close_pairs") *value = (int64_t)ctx->last_hash_close;

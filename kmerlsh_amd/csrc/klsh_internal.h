@@ -161,6 +161,9 @@ struct MergeWork {
   uint32_t tail_nsmall;      // "tail_small_groups": k_merge_tail's small-run workgroups
   uint32_t wide_group_grid;  // "wide_group_grid": the wide-row group merges, per class
   uint32_t screen_grid;      // "small_screen_grid": the small-run screen's persistent launch
+  // "wide_gram": at d = 512 the group merges of runs of at least this many rows (8, 16, 32, 64)
+  // decide on the matrix cores; 0 = none
+  uint32_t wide_gram = 32;
   uint32_t small_screen = 1;  // "small_screen": 1 = screen the small runs on the fp16 image first
   // "tail_merge_rows": below this many positions every merge class runs in ONE launch
   // (k_merge_tail); 0 = the default 2^20 (tests lower it to reach the per-class launches)

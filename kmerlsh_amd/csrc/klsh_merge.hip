@@ -1344,21 +1344,14 @@ __device__ __forceinline__ void split8(const float* p, bool ok, bf16x8& hi, bf16
 // One wave: the decisions of rows [R*64, R*64+64) against rows [C*64, C*64+64) (C <= R; pairs
 // c < a only), ORed into the position-space matrix P (W words per row, both P[a] bit c and
 // P[c] bit a).  rowA(a) / rowB(c) give the rows (LDS or memory); D = d, a multiple of 16.
-template <int D, class RowA, class RowB>
-__device__ __forceinline__ void gram_tile(uint32_t R, uint32_t C, uint32_t b, RowA rowA, RowB rowB,
-                                          const float* sq, const Decider& dc, uint64_t* P, int W,
-                                          uint32_t* fb = nullptr) {
+// The bf16x3 products of rows [a0, a0+64) x [c0, c0+64) over KD columns, accumulated into acc:
+// rowA(a) / rowB(c) point at the columns to take (LDS or memory), KD a multiple of 16.
+template <int KD, class RowA, class RowB>
+__device__ __forceinline__ void gram_acc(uint32_t a0, uint32_t c0, uint32_t b, RowA rowA,
+                                         RowB rowB, f32x16 (&acc)[2][2]) {
   const uint32_t lane = __lane_id(), r = lane & 31u, h = lane >> 5;
-  const uint32_t a0 = R * 64u, c0 = C * 64u;
-  f32x16 acc[2][2];
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.0f;
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
+  for (int s = 0; s < KD / 16; ++s) {
     bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -1375,6 +1368,41 @@ __device__ __forceinline__ void gram_tile(uint32_t R, uint32_t C, uint32_t b, Ro
         acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[m], bh[n], acc[m][n], 0, 0, 0);
       }
   }
+}
+
+template <int D, class RowA, class RowB>
+__device__ __forceinline__ void gram_decide(uint32_t R, uint32_t C, uint32_t b,
+                                            const f32x16 (&acc)[2][2], RowA rowA, RowB rowB,
+                                            const float* sq, const Decider& dc, uint64_t* P,
+                                            int W, uint32_t* fb);
+
+// One wave: the decisions of rows [R*64, R*64+64) against rows [C*64, C*64+64) (C <= R; pairs
+// c < a only), ORed into the position-space matrix P (W words per row, both P[a] bit c and
+// P[c] bit a).  rowA(a) / rowB(c) give the rows (LDS or memory); D = d, a multiple of 16.
+template <int D, class RowA, class RowB>
+__device__ __forceinline__ void gram_tile(uint32_t R, uint32_t C, uint32_t b, RowA rowA, RowB rowB,
+                                          const float* sq, const Decider& dc, uint64_t* P, int W,
+                                          uint32_t* fb = nullptr) {
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.0f;
+  gram_acc<D>(R * 64u, C * 64u, b, rowA, rowB, acc);
+  gram_decide<D>(R, C, b, acc, rowA, rowB, sq, dc, P, W, fb);
+}
+
+// The decisions from accumulated Gram values (gram_acc): pre-screen against dc's margin, the
+// reference's sequential dot over D columns (rowA / rowB: whole rows) for the close calls.
+template <int D, class RowA, class RowB>
+__device__ __forceinline__ void gram_decide(uint32_t R, uint32_t C, uint32_t b,
+                                            const f32x16 (&acc)[2][2], RowA rowA, RowB rowB,
+                                            const float* sq, const Decider& dc, uint64_t* P,
+                                            int W, uint32_t* fb) {
+  const uint32_t lane = __lane_id(), r = lane & 31u, h = lane >> 5;
+  const uint32_t a0 = R * 64u, c0 = C * 64u;
   // decisions: acc[m][n][i] is G[a][c] with a = a0 + 32m + (i&3) + 8(i>>2) + 4h, c = c0 + 32n + r;
   // bit e = 32m + 16n + i of hitm / ambm
   uint64_t hitm = 0ull, ambm = 0ull;
@@ -2940,7 +2968,10 @@ __device__ __forceinline__ float dot_acc_reg(float s, const float (&a)[N], const
   return s;
 }
 
-template <int G>
+// DG: d at compile time for the runs of G >= 8 rows (their pairwise decisions from one 64x64
+// MFMA Gram tile, certified with the wide margin the caller's decider carries, exact chains only
+// for the close calls), 0 = every pair by its exact chain.
+template <int G, int DG = 0>
 __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_t slot,
                                                  uint32_t* slots, const Decider& dc,
                                                  const Rows& r, float* tile, uint32_t* dlist,
@@ -2963,6 +2994,41 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
     return j >= b ? j - b : j;
   };
 
+  uint64_t full = 0ull;
+  if constexpr (DG > 0 && G >= 8) {
+    // 1'. the batch's decisions from one Gram tile on the matrix cores (bf16x3): the 64 lanes'
+    //     rows against each other, accumulated over the same LDS-staged 64-column chunks, pairs
+    //     across runs masked off afterwards; close calls by the exact chain (gram_decide)
+    __shared__ uint64_t Pw[64];  // position masks
+    __shared__ uint32_t sl[64];
+    __shared__ float sqs[64];
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.0f;
+    for (int c0 = 0; c0 < DG; c0 += kWideKC) {
+      wave_lds_fence();  // the previous chunk's reads are done
+      stage_chunk(r.x, dp, slot, valid, c0, kWideKC, tile);
+      wave_lds_fence();
+      auto rl = [&](uint32_t a) -> const float* { return tile + a * ST; };
+      gram_acc<kWideKC>(0u, 0u, 64u, rl, rl, acc);
+    }
+    wave_lds_fence();
+    Pw[lane] = 0ull;
+    sl[lane] = slot;  // (a lane past its run holds a valid row: slot 0)
+    sqs[lane] = valid ? sq : 1.0f;
+    wave_lds_fence();
+    auto rm = [&](uint32_t a) -> const float* { return r.x + (size_t)sl[a] * dp; };
+    gram_decide<DG>(0u, 0u, 64u, acc, rm, rm, sqs, dc, Pw, 1, nullptr);
+    __builtin_amdgcn_s_waitcnt(0x0070);  // (its atomics into LDS) vmcnt(0) lgkmcnt(0)
+    wave_lds_fence();
+    const uint64_t runbits = b >= 64u ? ~0ull : ((1ull << b) - 1ull);
+    full = valid ? ((Pw[lane] >> gbase) & runbits & ~(1ull << g)) : 0ull;
+    wave_lds_fence();
+  } else {
   // 1. every pairwise dot product of the run, chunk by chunk (lane g vs positions g + k)
   float acc[NK];
 #pragma unroll
@@ -2987,7 +3053,6 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
           acc[k - 1] = dot_acc_mem(acc[k - 1], mine, tile + (gbase + partner(k)) * ST, n);
     }
   }
-  uint64_t full = 0ull;
 #pragma unroll
   for (int k = 1; k <= NK; ++k) {
     if ((uint32_t)k <= kmax) {  // wave-uniform
@@ -3001,6 +3066,7 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
         full |= (uint64_t)in << src;
       }
     }
+  }
   }
 
   // member counts and list ends only for the runs with a matching pair (as merge_batch)
@@ -3080,7 +3146,7 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
   lds_fence();
 }
 
-template <int G>
+template <int G, int DG = 0>
 __global__ __launch_bounds__(64) void k_merge_group_wide(const uint2* __restrict__ list,
                                                          const uint32_t* count_ptr,
                                                          uint32_t* __restrict__ slots, Decider dc,
@@ -3096,7 +3162,7 @@ __global__ __launch_bounds__(64) void k_merge_group_wide(const uint2* __restrict
     const uint32_t k = bi * NG + grp;
     const uint2 e = k < n ? list[k] : make_uint2(0u, 0u);
     const uint32_t slot = g < e.y ? slots[e.x + g] : 0u;
-    merge_batch_wide<G>(e.x, e.y, slot, slots, dc, r, tile, dlist, ctr);
+    merge_batch_wide<G, DG>(e.x, e.y, slot, slots, dc, r, tile, dlist, ctr);
   }
   kt_end(kt, KC_SMALL);
 }
@@ -3587,6 +3653,16 @@ static void launch_big_wide(const MergeWork& w, int c, uint32_t* slots, const De
   k_merge_big_wide<RB, NT, KC><<<g, NT, lds, s>>>(w, c, slots, dc, r, ctr);
 }
 
+// |G - dot_ref| / (|a||b|) for the bf16x3 Gram value at width d against the reference's sequential
+// f32 dot: split residuals 3.03 * 2^-16, the MFMA's f32 sums (16 internal adds + one per chained
+// MFMA, three per k-step, at 2u), the reference's own (d + 1) * 2^-24 and the approximate quotient
+// (4 * 2^-24), with 1.5x headroom (kGramMargin, 1e-4, covers d <= 64; at d = 512 this is 1.37e-4).
+static float wide_gram_margin(int d) {
+  const float ks = (float)((d + 15) / 16);
+  return 1.5f * (3.03f * 0x1p-16f + (17.0f + 3.0f * ks) * 0x1p-23f + (float)(d + 1) * 0x1p-24f +
+                 4.0f * 0x1p-24f);
+}
+
 static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc,
                                const MergeWork& w, Counters* ctr, uint32_t n, hipStream_t s) {
   auto grid = [&](int c, uint32_t per_wave) {
@@ -3632,17 +3708,31 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
       screen(k_small_screen_wide<2, 0>, 0, 32);
     }
   }
-  auto group = [&](auto kern, int c, uint32_t per_wave) {
+  // runs of 8..64 rows at d = 512 (C5): pairwise decisions on the matrix cores (option
+  // wide_gram) with the margin of the bf16x3 Gram value at this width (wide_gram_margin)
+  const bool gram = w.wide_gram && dc.fast && r.d == 512;
+  const uint32_t gmin = w.wide_gram;  // the smallest group width that decides on the matrix cores
+  Decider dg = dc;
+  if (gram) {
+    const float m = wide_gram_margin(r.d);
+    dg.g_lo = dc.s_star - m;
+    dg.g_hi = dc.s_star + m;
+  }
+  auto group = [&](auto kern, int c, uint32_t per_wave, const Decider& dd) {
     kern<<<grid(c, per_wave), 64, 0, sl>>>(scr ? w.act[c] : w.cls[c],
-                                           scr ? &rc->n_act[c].v : &rc->n_cls[c].v, slots, dc, r,
+                                           scr ? &rc->n_act[c].v : &rc->n_cls[c].v, slots, dd, r,
                                            ctr, w.dlist, w.kt);
   };
-  group(k_merge_group_wide<64>, 5, 1);
-  group(k_merge_group_wide<32>, 4, 2);
-  group(k_merge_group_wide<16>, 3, 4);
-  group(k_merge_group_wide<8>, 2, 8);
-  group(k_merge_group_wide<4>, 1, 16);
-  group(k_merge_group_wide<2>, 0, 32);
+  if (gram && gmin <= 64) group(k_merge_group_wide<64, 512>, 5, 1, dg);
+  else group(k_merge_group_wide<64>, 5, 1, dc);
+  if (gram && gmin <= 32) group(k_merge_group_wide<32, 512>, 4, 2, dg);
+  else group(k_merge_group_wide<32>, 4, 2, dc);
+  if (gram && gmin <= 16) group(k_merge_group_wide<16, 512>, 3, 4, dg);
+  else group(k_merge_group_wide<16>, 3, 4, dc);
+  if (gram && gmin <= 8) group(k_merge_group_wide<8, 512>, 2, 8, dg);
+  else group(k_merge_group_wide<8>, 2, 8, dc);
+  group(k_merge_group_wide<4>, 1, 16, dc);
+  group(k_merge_group_wide<2>, 0, 32, dc);
 }
 
 void launch_runs(const uint32_t* key, uint32_t lo, uint32_t n, int bucket_thr, const MergeWork& w,

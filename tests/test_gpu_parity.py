@@ -508,6 +508,26 @@ def test_wide_small_screen_vs_oracle(engine, oracle, d, screen):
     assert_same_result(got, *want[:3])
 
 
+@pytest.mark.parametrize("gram", [8, 32, 0])
+def test_wide_gram_group_merges_vs_oracle(engine, oracle, gram):
+    """C5-width (d = 512) group merges with their pairwise decisions from the bf16x3 Gram tile
+    (option wide_gram, certified with the width's own margin) or from the exact chains: same
+    trace, counter and result as the oracle, special rows (huge, tiny, zero, NaN) included."""
+    rng = np.random.default_rng(512 + gram)
+    rows = clustered(rng, 30000, 512, 900, 0.05)
+    rows[5] *= np.float32(1e20)
+    rows[11] *= np.float32(1e-20)
+    rows[13] = 0.0
+    rows[17, 2] = np.nan
+    want = oracle.cluster(rows, 0.8, 4, 1000000, 31, 4)
+    with options(engine, wide_gram=gram, tail_merge_rows=1):
+        engine.load_rows(rows)
+        trace, counter, _ = engine.cluster(0.8, 4, 1000000, 31, 4)
+        got = engine.result()
+    assert np.array_equal(trace, want[3]) and counter == want[4]
+    assert_same_result(got, *want[:3])
+
+
 @pytest.mark.parametrize("b", [2, 3, 5, 9, 17, 33, 64])
 def test_small_screen_pcluster_special_rows(engine, oracle, b):
     """One small run through the screen (pcluster: the rows as one bucket) with a row the fp16
