@@ -1806,6 +1806,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->pw.wide_h16 = (uint32_t)value;
     return 0;
   }
+  if (n == "wide_unrolled") {
+    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_unrolled must be 0 or 1");
+    ctx->pw.wide_rolled = value ? 0u : 1u;
+    return 0;
+  }
   if (n == "long_runs") {
     if (value != 0 && value != 1 && value != 4) return fail(KLSH_E_ARG, "long_runs must be 0, 1 or 4");
     ctx->mw.long_off = value == 1 ? 0u : value == 0 ? 1u : 4u;
@@ -1874,6 +1879,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "long_runs") *value = ctx->mw.long_off == 1u ? 0 : ctx->mw.long_off == 0u ? 1 : ctx->mw.long_off;
   else if (n == "wide_projection") *value = ctx->pw.wide_h16;
   else if (n == "wide_gram") *value = ctx->mw.wide_gram;
+  else if (n == "wide_unrolled") *value = ctx->pw.wide_rolled ? 0 : 1;
   else if (n == "fp16_image") *value = ctx->rows.xh != nullptr;
   else if (n == "last_hash_kernel") *value = ctx->last_hash_kernel;
   else if (n == "last_hash_close_pairs") *value = (int64_t)ctx->last_hash_close;

@@ -236,6 +236,7 @@ struct ProjectWork {
   uint32_t segcap;     // "h16_segcap" (tests): fix-up entries per fp16-projection workgroup
   uint32_t variant;    // "projection": kProjAuto / kProjPacked / kProjScreen (set per launch)
   uint32_t wide_h16;   // "wide_projection": 1 = wide rows projected from the fp16 image
+  uint32_t wide_rolled;  // "wide_unrolled" = 0: d = 512 through the generic wide screen
 };
 // Projection variants (klsh_set_option "projection"): the default picks the certified
 // matrix-core screen where it exists (the fp16 row image at d = 16 / 32 / 64, bf16x3 above 64)

@@ -545,7 +545,14 @@ __device__ __forceinline__ void hsplit8(float4 u, float4 v, wh16x8& hi, wh16x8& 
   }
 }
 
-__global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __restrict__ X, int d, int dp,
+// DT > 0: d == DT (a multiple of 64), every row load unconditional and the round loop unrolled,
+// so each round waits only for its own loads (vmcnt counts, not vmcnt(0)) and the next round's
+// stay in flight behind the math; KLSH_WIDE_PF rounds are kept ahead (1 or 2).
+#ifndef KLSH_WIDE_PF
+#define KLSH_WIDE_PF 1
+#endif
+template <int DT>
+__global__ __launch_bounds__(kWideNT, 2) void k_project_mfma_wide(const float* __restrict__ X, int d, int dp,
                                                            const uint32_t* __restrict__ slots,
                                                            uint32_t* __restrict__ keys, uint32_t n,
                                                            const float* __restrict__ W, int h,
@@ -605,6 +612,42 @@ __global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __re
         dst[q][1] = k0 + 8 <= dp ? *reinterpret_cast<const float4*>(xr + k0 + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     };
+    if constexpr (DT > 0) {
+      constexpr int R = DT / 64, PF = KLSH_WIDE_PF, NB = PF + 1;
+      float4 xb[NB][4][2];
+      auto load_full = [&](int rd, float4 (&dst)[4][2]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k0 = 64 * rd + 16 * q + 8 * (int)hh;
+          dst[q][0] = *reinterpret_cast<const float4*>(xr + k0);
+          dst[q][1] = *reinterpret_cast<const float4*>(xr + k0 + 4);
+        }
+      };
+#pragma unroll
+      for (int rd = 0; rd < PF && rd < R; ++rd) load_full(rd, xb[rd % NB]);
+#pragma unroll
+      for (int rd = 0; rd < R; ++rd) {
+        if (rd + PF < R) load_full(rd + PF, xb[(rd + PF) % NB]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 u = xb[rd % NB][q][0], v = xb[rd % NB][q][1];
+          wh16x8 ah, al, aa;
+          hsplit8(u, v, ah, al, aa);
+          ss += u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w + v.x * v.x + v.y * v.y + v.z * v.z +
+                v.w * v.w;
+          const int sk = 4 * rd + q;
+          const wh16x8 bh = bfr[2 * (sk * 64 + lane)], bl = bfr[2 * (sk * 64 + lane) + 1];
+          wh16x8 ba;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ba[e] = __builtin_fabsf16(bh[e]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+          aab = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa, ba, aab, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keeps the loads PF rounds ahead, not all hoisted
+      }
+    } else {
     load_round(0, xa);
     for (int s0 = 0; s0 < KS; s0 += 4) {
       if (s0 + 4 < KS) load_round(s0 + 4, xn4);
@@ -631,6 +674,7 @@ __global__ __launch_bounds__(kWideNT) void k_project_mfma_wide(const float* __re
         xa[q][0] = xn4[q][0];
         xa[q][1] = xn4[q][1];
       }
+    }
     }
     ss += __shfl_xor(ss, 32, 64);
     const float xn = __builtin_amdgcn_sqrtf(ss) * 1.001f;
@@ -940,7 +984,9 @@ int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_
     const size_t flds = sizeof(float) * (size_t)h * r.dp;  // the fix-up kernel's hyperplanes
     if (lds <= 96 * 1024 && flds <= 128 * 1024) {
       static const bool lds_ok =
-          hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_mfma_wide),
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_mfma_wide<0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_mfma_wide<512>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
           hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_h16_wide),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
@@ -960,10 +1006,14 @@ int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_
         k_project_h16_wide<<<gm, dim3(kWideNT), lds, s>>>(r.xh, r.d, r.dp, slots, keys, n, r.x, W,
                                                           h, key_or, h16_eps(r.d), h16_abs(r.d),
                                                           *pw, kt);
+      else if (r.d == 512 && !pw->wide_rolled)  // option "wide_unrolled" (default 1)
+        k_project_mfma_wide<512><<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W,
+                                                                h, key_or, wide_eps(r.d),
+                                                                wide_abs(r.d), *pw, kt);
       else
-        k_project_mfma_wide<<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h,
-                                                           key_or, wide_eps(r.d), wide_abs(r.d),
-                                                           *pw, kt);
+        k_project_mfma_wide<0><<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W, h,
+                                                              key_or, wide_eps(r.d), wide_abs(r.d),
+                                                              *pw, kt);
       const uint32_t fcap = pw->fix_grid ? std::max(16u, pw->fix_grid) : 1024u;  // "fix_grid"
       k_project_fix<<<fcap, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
       return r.xh && pw->wide_h16 ? kPkWideH16 : kPkWide;
