@@ -328,9 +328,12 @@ float h16_abs(int d) { return 1.5f * 2.0f * 0x1p-25f * std::sqrt((float)d); }
 // per listed row: the f32 row loaded once, the reference's sequential chain (hash/lshash.cc:44-51,
 // mul then add, never fused) per flagged hyperplane from the f32 hyperplanes in LDS.
 typedef _Float16 ph16x2 __attribute__((ext_vector_type(2)));
+#ifndef KLSH_H16_PIPE
+#define KLSH_H16_PIPE 0
+#endif
 
 template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_project_h16(const uint16_t* __restrict__ XH,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KLSH_H16_PIPE ? 3 : 4))) void k_project_h16(const uint16_t* __restrict__ XH,
                                                      const float* __restrict__ X, int dp,
                                                      const uint32_t* __restrict__ slots,
                                                      uint32_t* __restrict__ keys, uint32_t n,
@@ -382,16 +385,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const uint32_t wv = t >> 6;
   const uint32_t step = gridDim.x * 256u;
   uint32_t g0 = (blockIdx.x * 4u + wv) * 64u;
-  uint32_t sl = g0 + lane < n ? slots[g0 + lane] : 0u;
   uint4* seg = reinterpret_cast<uint4*>(pw.fix) + (size_t)blockIdx.x * segcap;
-  for (; g0 < n; g0 += step) {
-    ph16x8 xr[2 * KS];  // the lane's row, 8 columns per chunk
-    {
-      const uint16_t* src = XH + (size_t)sl * dp;
-#pragma unroll
-      for (int c = 0; c < 2 * KS; ++c) xr[c] = *reinterpret_cast<const ph16x8*>(src + 8 * c);
-    }
-    sl = g0 + step + lane < n ? slots[g0 + step + lane] : 0u;  // the next iteration's slot
+  auto group = [&](const ph16x8 (&xr)[2 * KS], uint32_t g0) __attribute__((always_inline)) {
     float ss = 0.0f;  // |x~|^2 of the lane's row (a bound only)
 #pragma unroll
     for (int c = 0; c < 2 * KS; ++c)
@@ -471,7 +466,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       // hyperplane 0 is the key's most significant bit
       if (done) keys[row] = (h > 0 ? (__builtin_bitreverse32(key_bits) >> (32 - h)) : 0u) | key_or;
     }
+  };
+#if KLSH_H16_PIPE
+  // two row buffers in turn: group g + 1's rows load while group g decides, so a wave keeps its
+  // loads in flight through the math (no buffer copies).  Every load is unconditional (lanes past
+  // n read slots[0]'s row) and a slot is read two groups ahead, before the rows that precede its
+  // use, so each wait is a count (vmcnt(9)), never a drain of the rows in flight.
+  auto slot_at = [&](uint32_t g) { return slots[g + lane < n ? g + lane : 0u]; };
+  auto load_rows = [&](ph16x8 (&xr)[2 * KS], uint32_t sl) __attribute__((always_inline)) {
+    const uint16_t* src = XH + (size_t)sl * dp;
+#pragma unroll
+    for (int c = 0; c < 2 * KS; ++c) xr[c] = *reinterpret_cast<const ph16x8*>(src + 8 * c);
+  };
+  ph16x8 xa[2 * KS], xb[2 * KS];
+  uint32_t s0 = slot_at(g0), s1 = slot_at(g0 + step);
+  load_rows(xa, s0);
+  s0 = slot_at(g0 + 2 * step);
+  for (; g0 < n; g0 += 2 * step) {
+    const uint32_t s3 = slot_at(g0 + 3 * step);
+    load_rows(xb, s1);
+    s1 = s3;
+    group(xa, g0);
+    if (g0 + step >= n) break;
+    const uint32_t s4 = slot_at(g0 + 4 * step);
+    load_rows(xa, s0);
+    s0 = s4;
+    group(xb, g0 + step);
   }
+#else
+  uint32_t sl = g0 + lane < n ? slots[g0 + lane] : 0u;
+  for (; g0 < n; g0 += step) {
+    ph16x8 xr[2 * KS];  // the lane's row, 8 columns per chunk
+    {
+      const uint16_t* src = XH + (size_t)sl * dp;
+#pragma unroll
+      for (int c = 0; c < 2 * KS; ++c) xr[c] = *reinterpret_cast<const ph16x8*>(src + 8 * c);
+    }
+    sl = g0 + step + lane < n ? slots[g0 + step + lane] : 0u;  // the next iteration's slot
+    group(xr, g0);
+  }
+#endif
   __syncthreads();
   // the close calls of this workgroup's rows
   const uint32_t cnt = min(s_cnt, segcap);
