@@ -2933,26 +2933,34 @@ static void launch_huge(const MergeWork& w, uint32_t* slots, const Decider& dc, 
 // reference's k order), and the walk's recomputations read the two rows from memory.
 constexpr int kWideKC = 64;
 
-// Columns [c0, c0 + kcp) of the 64 lanes' rows -> LDS rows (stride kWideKC + 4), coalesced:
-// 16 lanes per row, 4 rows per wave instruction.  kcp is a multiple of 4.
+// The exact group merges' chunk width (C5: 32 columns halve the staged tile to 9 KB per wave, so
+// LDS no longer caps the waves per CU below what the registers allow)
+#ifndef KLSH_WIDE_EXACT_KC
+#define KLSH_WIDE_EXACT_KC 32
+#endif
+constexpr int kWideXKC = KLSH_WIDE_EXACT_KC;
+
+// Columns [c0, c0 + kcp) of the 64 lanes' rows -> LDS rows (stride KC + 4), coalesced:
+// KC/4 lanes per row, 256/KC rows per wave instruction.  kcp is a multiple of 4.
+template <int KC = kWideKC>
 __device__ __forceinline__ void stage_chunk(const float* __restrict__ X, int dp, uint32_t slot,
                                             bool valid, int c0, int kcp, float* tile) {
-  constexpr int ST = kWideKC + 4;
+  constexpr int ST = KC + 4, LPR = KC / 4, RPI = 64 / LPR;
   const uint32_t lane = __lane_id();
-  const uint32_t q = lane & 15u, rsub = lane >> 4;
+  const uint32_t q = lane & (LPR - 1u), rsub = lane / LPR;
   const bool col_ok = (int)(4 * q) < kcp;
-  float4 v[16];
+  float4 v[LPR];
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const uint32_t row = it * 4 + rsub;
+  for (int it = 0; it < LPR; ++it) {
+    const uint32_t row = it * RPI + rsub;
     const uint32_t s = shfl32(slot, row);
     const int ok = __shfl(valid ? 1 : 0, (int)row, 64);
     v[it] = (ok && col_ok) ? *reinterpret_cast<const float4*>(X + (size_t)s * dp + c0 + 4 * q)
                            : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
 #pragma unroll
-  for (int it = 0; it < 16; ++it)
-    if (col_ok) *reinterpret_cast<float4*>(tile + (it * 4 + rsub) * ST + 4 * q) = v[it];
+  for (int it = 0; it < LPR; ++it)
+    if (col_ok) *reinterpret_cast<float4*>(tile + (it * RPI + rsub) * ST + 4 * q) = v[it];
 }
 
 template <int N>
@@ -3030,27 +3038,28 @@ __device__ __forceinline__ void merge_batch_wide(uint32_t p, uint32_t b, uint32_
     wave_lds_fence();
   } else {
   // 1. every pairwise dot product of the run, chunk by chunk (lane g vs positions g + k)
+  constexpr int XKC = kWideXKC, XST = XKC + 4;
   float acc[NK];
 #pragma unroll
   for (int k = 0; k < NK; ++k) acc[k] = 0.0f;
-  for (int c0 = 0; c0 < d; c0 += kWideKC) {
-    const int n = min(kWideKC, d - c0), kcp = min(kWideKC, dp - c0);
+  for (int c0 = 0; c0 < d; c0 += XKC) {
+    const int n = min(XKC, d - c0), kcp = min(XKC, dp - c0);
     wave_lds_fence();  // the previous chunk's reads are done
-    stage_chunk(r.x, dp, slot, valid, c0, kcp, tile);
+    stage_chunk<XKC>(r.x, dp, slot, valid, c0, kcp, tile);
     wave_lds_fence();
-    const float* mine = tile + lane * ST;
-    if (n == kWideKC) {
-      float x[kWideKC];
-      load_row<kWideKC>(mine, x);
+    const float* mine = tile + lane * XST;
+    if (n == XKC) {
+      float x[XKC];
+      load_row<XKC>(mine, x);
 #pragma unroll
       for (int k = 1; k <= NK; ++k)
         if ((uint32_t)k <= kmax && valid && (uint32_t)k <= half)
-          acc[k - 1] = dot_acc_reg<kWideKC>(acc[k - 1], x, tile + (gbase + partner(k)) * ST);
+          acc[k - 1] = dot_acc_reg<XKC>(acc[k - 1], x, tile + (gbase + partner(k)) * XST);
     } else {
 #pragma unroll
       for (int k = 1; k <= NK; ++k)
         if ((uint32_t)k <= kmax && valid && (uint32_t)k <= half)
-          acc[k - 1] = dot_acc_mem(acc[k - 1], mine, tile + (gbase + partner(k)) * ST, n);
+          acc[k - 1] = dot_acc_mem(acc[k - 1], mine, tile + (gbase + partner(k)) * XST, n);
     }
   }
 #pragma unroll
@@ -3152,7 +3161,7 @@ __global__ __launch_bounds__(64) void k_merge_group_wide(const uint2* __restrict
                                                          uint32_t* __restrict__ slots, Decider dc,
                                                          Rows r, Counters* ctr, uint32_t* dlist,
                                                          KTime kt) {
-  __shared__ __attribute__((aligned(16))) float tile[64 * (kWideKC + 4)];
+  __shared__ __attribute__((aligned(16))) float tile[64 * ((DG > 0 && G >= 8 ? kWideKC : kWideXKC) + 4)];
   constexpr uint32_t NG = 64 / G;
   kt_begin(kt, KC_SMALL);
   const uint32_t n = __hip_atomic_load(count_ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
