@@ -3337,11 +3337,14 @@ __global__ __launch_bounds__(64) void k_small_screen_wide(const uint2* __restric
 // position space (as k_merge_big).  A 64x64 decision tile is one wave's job: its 64 rows'
 // chains (one per lane, 64 columns each) run over KC-column chunks, the column block's chunk
 // staged in the wave's own LDS region and read by broadcast.
+#ifndef KLSH_BIGWIDE_GLDS
+#define KLSH_BIGWIDE_GLDS 1
+#endif
 template <int RB, int NT, int KC>
 struct BigWideLayout {
   static constexpr int W = RB / 64;
   static constexpr int NW = NT / 64;
-  static constexpr int STB = KC + 4;
+  static constexpr int STB = KC;  // unpadded: the tile is filled lane-linearly (and read by broadcast)
   static constexpr size_t tiles = 0;
   static constexpr size_t P = tiles + sizeof(float) * NW * 64 * STB;
   static constexpr size_t meta = P + sizeof(uint64_t) * RB * W;
@@ -3402,7 +3405,7 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(MergeWork w, int cls,
       const uint32_t C = ti - R * (R + 1) / 2;
       const uint32_t a = R * 64u + lane;
       const bool va = a < b;
-      const float* xa = va ? row_ptr(a) : nullptr;
+      const float* xa = row_ptr(va ? a : 0u);  // (a lane past the run reads row 0, unused)
       const uint32_t c0 = C * 64u, c1 = min(b, c0 + 64u);
       float acc[64];
 #pragma unroll
@@ -3410,19 +3413,35 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(MergeWork w, int cls,
       for (int k0 = 0; k0 < d; k0 += KC) {
         const int n = min(KC, d - k0), kcp = min(KC, dp - k0);
         lds_fence();
-        for (uint32_t q = lane; q < 64u * (uint32_t)(kcp / 4); q += 64) {
-          const uint32_t row = q / (uint32_t)(kcp / 4), e4 = q % (uint32_t)(kcp / 4);
-          if (c0 + row < c1)
-            *reinterpret_cast<float4*>(ctile + row * STB + 4 * e4) =
-                *reinterpret_cast<const float4*>(r.x + (size_t)slot[c0 + row] * dp + k0 + 4 * e4);
+        if (KLSH_BIGWIDE_GLDS && kcp == KC) {
+          // a full chunk straight into LDS (global_load_lds, 16 B a lane: the tile is unpadded, so
+          // instruction i fills floats [256 i, 256 i + 256) lane-linearly) — no registers, every
+          // load in flight at once; rows past the run read row c0 (never read back)
+          constexpr uint32_t PER = KC / 4;
+#pragma unroll
+          for (uint32_t i = 0; i < PER; ++i) {
+            const uint32_t q = lane + 64u * i, row = q / PER, e4 = q % PER;
+            const uint32_t sr = slot[c0 + row < c1 ? c0 + row : c0];
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(r.x + (size_t)sr * dp + k0 + 4 * e4),
+                (__attribute__((address_space(3))) void*)(ctile + 256u * i), 16, 0, 0);
+          }
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the tile has landed
+        } else {
+          for (uint32_t q = lane; q < 64u * (uint32_t)(kcp / 4); q += 64) {
+            const uint32_t row = q / (uint32_t)(kcp / 4), e4 = q % (uint32_t)(kcp / 4);
+            if (c0 + row < c1)
+              *reinterpret_cast<float4*>(ctile + row * STB + 4 * e4) =
+                  *reinterpret_cast<const float4*>(r.x + (size_t)slot[c0 + row] * dp + k0 + 4 * e4);
+          }
         }
         lds_fence();
         if (n == KC) {
           float x[KC];
 #pragma unroll
           for (int k = 0; k < KC; k += 4) {
-            const float4 v = va ? *reinterpret_cast<const float4*>(xa + k0 + k)
-                                : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            float4 v = *reinterpret_cast<const float4*>(xa + k0 + k);
+            if (!va) v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             x[k] = v.x; x[k + 1] = v.y; x[k + 2] = v.z; x[k + 3] = v.w;
           }
 #pragma unroll
