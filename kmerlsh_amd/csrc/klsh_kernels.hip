@@ -328,12 +328,9 @@ float h16_abs(int d) { return 1.5f * 2.0f * 0x1p-25f * std::sqrt((float)d); }
 // per listed row: the f32 row loaded once, the reference's sequential chain (hash/lshash.cc:44-51,
 // mul then add, never fused) per flagged hyperplane from the f32 hyperplanes in LDS.
 typedef _Float16 ph16x2 __attribute__((ext_vector_type(2)));
-#ifndef KLSH_H16_PIPE
-#define KLSH_H16_PIPE 0
-#endif
 
 template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KLSH_H16_PIPE ? 3 : 4))) void k_project_h16(const uint16_t* __restrict__ XH,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_project_h16(const uint16_t* __restrict__ XH,
                                                      const float* __restrict__ X, int dp,
                                                      const uint32_t* __restrict__ slots,
                                                      uint32_t* __restrict__ keys, uint32_t n,
@@ -356,16 +353,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KLSH_H16_PI
     if (woff_dev) W += (size_t)*woff_dev * dp;
   }
   const uint32_t t = threadIdx.x, lane = t & 63u, hh = lane >> 5;
-  for (int e = (int)t; e < 32 * D; e += 256) {
-    const int j = e / D, k = e % D;
-    swf[e] = j < h ? W[(size_t)j * dp + k] : 0.0f;
+  const uint32_t wv = t >> 6;
+  const uint32_t step = gridDim.x * 256u;
+  uint32_t g0 = (blockIdx.x * 4u + wv) * 64u;
+  // the wave's first rows are requested before the hyperplanes are staged, so their latency
+  // overlaps the staging (a launch of a few hundred thousand rows is one or two groups a wave);
+  // loads are unconditional (a lane past n reads slots[0]'s row, unused)
+  auto load_rows = [&](ph16x8 (&xr)[2 * KS], uint32_t sl) __attribute__((always_inline)) {
+    const uint16_t* src = XH + (size_t)sl * dp;
+#pragma unroll
+    for (int c = 0; c < 2 * KS; ++c) xr[c] = *reinterpret_cast<const ph16x8*>(src + 8 * c);
+  };
+  // the hyperplane loads and the slot load are issued together (one round trip, not one per
+  // element), then the rows, whose latency the LDS staging below overlaps
+  constexpr int NWL = 32 * D / 256;
+  float wl[NWL];
+#pragma unroll
+  for (int i = 0; i < NWL; ++i) {
+    const int e = (int)t + 256 * i, j = e / D, k = e % D;
+    wl[i] = W[(size_t)(j < h ? j : 0) * dp + k];
+  }
+  const uint32_t sl0 = slots[g0 + lane < n ? g0 + lane : 0u];
+  __builtin_amdgcn_sched_barrier(0);  // (keeps every hyperplane load ahead of the row loads)
+  ph16x8 xr[2 * KS];  // the lane's row, 8 columns per chunk
+  load_rows(xr, sl0);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < NWL; ++i) {
+    const int e = (int)t + 256 * i;
+    swf[e] = e / D < h ? wl[i] : 0.0f;
   }
   if (t == 0) s_cnt = s_close = 0u;
   __syncthreads();
-  if (t < 32) {
+  {  // |w_j|: 8 lanes per hyperplane (a bound: any summation order, the hardware sqrt, x 1.001)
+    const int j = (int)(t >> 3), p = (int)(t & 7u);
     float a = 0.0f;
-    for (int k = 0; k < D; ++k) a += swf[t * D + k] * swf[t * D + k];
-    swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;  // a bound: the hardware sqrt (1 ulp) suffices
+#pragma unroll
+    for (int k = p; k < D; k += 8) a += swf[j * D + k] * swf[j * D + k];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    a += __shfl_xor(a, 4, 64);
+    if (p == 0) swn[j] = __builtin_amdgcn_sqrtf(a) * 1.001f;
   }
   // A fragment of lane L at k-step s: hyperplane L & 31, columns 16s + 8(L >> 5) + 0..7, split
   for (int e = (int)t; e < KS * 64; e += 256) {
@@ -382,9 +410,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KLSH_H16_PI
     sa[1][sk][L] = lo8;
   }
   __syncthreads();
-  const uint32_t wv = t >> 6;
-  const uint32_t step = gridDim.x * 256u;
-  uint32_t g0 = (blockIdx.x * 4u + wv) * 64u;
   uint4* seg = reinterpret_cast<uint4*>(pw.fix) + (size_t)blockIdx.x * segcap;
   auto group = [&](const ph16x8 (&xr)[2 * KS], uint32_t g0) __attribute__((always_inline)) {
     float ss = 0.0f;  // |x~|^2 of the lane's row (a bound only)
@@ -467,45 +492,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KLSH_H16_PI
       if (done) keys[row] = (h > 0 ? (__builtin_bitreverse32(key_bits) >> (32 - h)) : 0u) | key_or;
     }
   };
-#if KLSH_H16_PIPE
-  // two row buffers in turn: group g + 1's rows load while group g decides, so a wave keeps its
-  // loads in flight through the math (no buffer copies).  Every load is unconditional (lanes past
-  // n read slots[0]'s row) and a slot is read two groups ahead, before the rows that precede its
-  // use, so each wait is a count (vmcnt(9)), never a drain of the rows in flight.
-  auto slot_at = [&](uint32_t g) { return slots[g + lane < n ? g + lane : 0u]; };
-  auto load_rows = [&](ph16x8 (&xr)[2 * KS], uint32_t sl) __attribute__((always_inline)) {
-    const uint16_t* src = XH + (size_t)sl * dp;
-#pragma unroll
-    for (int c = 0; c < 2 * KS; ++c) xr[c] = *reinterpret_cast<const ph16x8*>(src + 8 * c);
-  };
-  ph16x8 xa[2 * KS], xb[2 * KS];
-  uint32_t s0 = slot_at(g0), s1 = slot_at(g0 + step);
-  load_rows(xa, s0);
-  s0 = slot_at(g0 + 2 * step);
-  for (; g0 < n; g0 += 2 * step) {
-    const uint32_t s3 = slot_at(g0 + 3 * step);
-    load_rows(xb, s1);
-    s1 = s3;
-    group(xa, g0);
-    if (g0 + step >= n) break;
-    const uint32_t s4 = slot_at(g0 + 4 * step);
-    load_rows(xa, s0);
-    s0 = s4;
-    group(xb, g0 + step);
-  }
-#else
-  uint32_t sl = g0 + lane < n ? slots[g0 + lane] : 0u;
-  for (; g0 < n; g0 += step) {
-    ph16x8 xr[2 * KS];  // the lane's row, 8 columns per chunk
-    {
-      const uint16_t* src = XH + (size_t)sl * dp;
-#pragma unroll
-      for (int c = 0; c < 2 * KS; ++c) xr[c] = *reinterpret_cast<const ph16x8*>(src + 8 * c);
-    }
-    sl = g0 + step + lane < n ? slots[g0 + step + lane] : 0u;  // the next iteration's slot
+  while (g0 < n) {
+    const uint32_t sl = slots[g0 + step + lane < n ? g0 + step + lane : 0u];  // the next group's
     group(xr, g0);
+    g0 += step;
+    if (g0 >= n) break;
+    load_rows(xr, sl);
   }
-#endif
   __syncthreads();
   // the close calls of this workgroup's rows
   const uint32_t cnt = min(s_cnt, segcap);
@@ -1099,7 +1092,8 @@ __global__ __launch_bounds__(256) void k_compact_count(const uint32_t* __restric
 #pragma unroll
   for (int k = 0; k < kCompactTile / 256; ++k) {
     const uint32_t i = T0 + k * 256u + t;
-    c += (uint32_t)__popcll(__ballot(i < n && slots[i] != kInvalid));
+    const uint32_t v = slots[i < n ? i : 0u];  // unconditional: the tile's loads all in flight
+    c += (uint32_t)__popcll(__ballot(i < n && v != kInvalid));
   }
   if (lane == 0) wsum[wv] = c;
   __syncthreads();
@@ -1184,9 +1178,13 @@ __global__ __launch_bounds__(256) void k_compact_apply(const uint32_t* __restric
   uint32_t v[K];
   uint64_t m[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
+  for (int k = 0; k < K; ++k) {  // every load issued first (unconditional: one wait, not K)
     const uint32_t i = T0 + k * 256u + t;
-    v[k] = i < n ? slots[i] : kInvalid;
+    v[k] = slots[i < n ? i : 0u];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (T0 + k * 256u + t >= n) v[k] = kInvalid;
     m[k] = __ballot(v[k] != kInvalid);
     if (lane == 0) cnt[k * 4 + wv] = (uint32_t)__popcll(m[k]);
   }
@@ -1235,9 +1233,13 @@ __global__ __launch_bounds__(256) void k_compact_lb(const uint32_t* __restrict__
   uint64_t m[K];
   uint32_t mine = 0;
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
+  for (int k = 0; k < K; ++k) {  // every load issued first (unconditional: one wait, not K)
     const uint32_t i = T0 + k * 256u + t;
-    v[k] = i < n ? slots[i] : kInvalid;
+    v[k] = slots[i < n ? i : 0u];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (T0 + k * 256u + t >= n) v[k] = kInvalid;
     m[k] = __ballot(v[k] != kInvalid);
     mine += (uint32_t)__popcll(m[k]);
     if (lane == 0) cnt[k * 4 + wv] = (uint32_t)__popcll(m[k]);

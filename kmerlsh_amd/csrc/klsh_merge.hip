@@ -1032,27 +1032,58 @@ __global__ __launch_bounds__(256) void k_runs_scan(uint32_t* __restrict__ counts
   const uint32_t t = threadIdx.x;
   const uint32_t per = (ntiles + 255u) / 256u;
   const uint32_t a = min(ntiles, t * per), e = min(ntiles, a + per);
+  // A thread's tiles are read CH at a time, every load of a chunk issued before any use (index
+  // clamped into the chunk, no branch around a load): one round trip per chunk, not per tile —
+  // this one-workgroup-per-list launch is a latency chain.
+  constexpr uint32_t CH = 8;
   uint32_t fmin = ~0u;  // first head of this thread's tiles
-  for (uint32_t i = a; i < e; ++i) fmin = min(fmin, heads_fl[i].x);
+  for (uint32_t i0 = a; i0 < e; i0 += CH) {
+    uint32_t hx[CH];
+#pragma unroll
+    for (uint32_t c = 0; c < CH; ++c) hx[c] = heads_fl[min(i0 + c, e - 1u)].x;
+#pragma unroll
+    for (uint32_t c = 0; c < CH; ++c) fmin = min(fmin, hx[c]);  // (clamped repeats: harmless)
+  }
   uint32_t after = block_excl_suffix_min_256(fmin);  // first head after this thread's tiles
   uint32_t acc = 0;
-  for (uint32_t i = e; i-- > a;) {  // reverse: `after` is the first head after tile i
-    const uint2 hf = heads_fl[i];
-    const uint32_t te = min(after, n);
-    if (l == 0) tail_ends[i] = te;
-    const uint32_t b = last_run_len(i, hf.y, te);
-    uint32_t v = row[i];
-    if (b) v += run_contrib(l, run_class(b, bucket_thr), b);
-    row[i] = v;
-    acc += v;
-    after = min(after, hf.x);
+  for (uint32_t i1 = e; i1 > a;) {  // reverse: `after` is the first head after tile i
+    const uint32_t i0 = i1 - a > CH ? i1 - CH : a;
+    uint2 hf[CH];
+    uint32_t rv[CH];
+#pragma unroll
+    for (uint32_t c = 0; c < CH; ++c) {
+      const uint32_t j = min(i0 + c, i1 - 1u);
+      hf[c] = heads_fl[j];
+      rv[c] = row[j];
+    }
+#pragma unroll
+    for (int c = (int)CH - 1; c >= 0; --c) {
+      const uint32_t i = i0 + (uint32_t)c;
+      if (i < i1) {
+        const uint32_t te = min(after, n);
+        if (l == 0) tail_ends[i] = te;
+        const uint32_t b = last_run_len(i, hf[c].y, te);
+        uint32_t v = rv[c];
+        if (b) v += run_contrib(l, run_class(b, bucket_thr), b);
+        row[i] = v;
+        acc += v;
+        after = min(after, hf[c].x);
+      }
+    }
+    i1 = i0;
   }
   uint32_t total;
   uint32_t run = block_excl_scan_256(acc, &total);
-  for (uint32_t i = a; i < e; ++i) {
-    const uint32_t v = row[i];
-    row[i] = run;
-    run += v;
+  for (uint32_t i0 = a; i0 < e; i0 += CH) {
+    uint32_t rv[CH];
+#pragma unroll
+    for (uint32_t c = 0; c < CH; ++c) rv[c] = row[min(i0 + c, e - 1u)];
+#pragma unroll
+    for (uint32_t c = 0; c < CH; ++c)
+      if (i0 + c < e) {
+        row[i0 + c] = run;
+        run += rv[c];
+      }
   }
   if (t == 0) *run_counter(rc, l) = total;
 }
@@ -1169,11 +1200,15 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
   const uint32_t d = blockIdx.x;
   const uint32_t RAD = 1u << lb, MASK = RAD - 1u;
   // the bucket: [base, base + m) of the partition
+  // (every global load of this kernel is unconditional, index clamped into range: a load under a
+  // branch is waited for at once, and these few-hundred-key buckets are a chain of round trips)
   uint32_t part = 0;
+  const uint32_t m = dtot[d];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const uint32_t i = t * 4u + (uint32_t)q;
-    part += i < d ? dtot[i] : 0u;
+    const uint32_t x = dtot[i < d ? i : 0u];
+    part += i < d ? x : 0u;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
@@ -1186,13 +1221,22 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
   if (t < (uint32_t)kRunRows) lcnt[t] = 0u;
   __syncthreads();
   const uint32_t base = red[0] + red[1] + red[2] + red[3];
-  const uint32_t m = dtot[d];
   if (m == 0u) {
     kt_end(w.kt, KC_RUNS);
     return;
   }
-  // 1. low-digit counts
-  for (uint32_t i = t; i < m; i += 256) atomicAdd(&cnt[kin[base + i] & MASK], 1u);
+  // 1. low-digit counts (4 keys a thread per round, loads first)
+  for (uint32_t i0 = 0; i0 < m; i0 += 1024u) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t i = i0 + (uint32_t)q * 256u + t;
+      kk[q] = kin[base + (i < m ? i : 0u)];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (i0 + (uint32_t)q * 256u + t < m) atomicAdd(&cnt[kk[q] & MASK], 1u);
+  }
   __syncthreads();
   // 2. the runs (digits with a count >= 2) per list, and the digit starts
   uint32_t c4[4], acc = 0, heads = 0, small_rows = 0;
@@ -1262,8 +1306,8 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
 #pragma unroll
     for (int j = 0; j < (int)kItems; ++j) {
       const uint32_t p = r0 + wv * kWave + (uint32_t)j * 64u + lane;
-      k[j] = p < m ? kin[base + p] : 0u;
-      v[j] = p < m ? vin[base + p] : 0u;
+      k[j] = kin[base + (p < m ? p : 0u)];
+      v[j] = vin[base + (p < m ? p : 0u)];
     }
 #pragma unroll
     for (int j = 0; j < (int)kItems; ++j) {
