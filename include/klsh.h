@@ -184,6 +184,7 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *                      (Gram bit matrix + one walk step per merge); 1 = only runs over 896 rows;
  *                      0 = k_merge_huge for those
  *   "wide_projection"  1 = wide rows projected from the fp16 image (needs wide_image = 1)
+ *   "wide_unrolled"    1 (default) = d = 512 projected by the unrolled screen; 0 = the generic one
  *   "wide_gram"        at d = 512 the group merges of runs of at least this many rows (8, 16, 32
  *                      or 64; default 32) take their decisions from an MFMA Gram matrix with a
  *                      certified margin, the uncertain pairs from the exact chains; 0 = none
