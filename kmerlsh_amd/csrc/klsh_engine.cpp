@@ -1073,6 +1073,13 @@ static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, 
                        uint64_t* nt_trace, klsh_stats* st,
                        const std::function<klsh::KTime(uint64_t)>& ktime) {
   hipStream_t s = ctx->stream;
+#ifdef KLSH_MERGE_PROF
+  if (getenv("KLSH_MERGE_PROF")) {  // diagnostics: the head's merge profile apart from the tail's
+    fprintf(stderr, "[mprof] ---- head: iterations before %d\n", it);
+    klsh::merge_prof_dump(stderr);
+    fprintf(stderr, "[mprof] ---- tail: iterations %d..%d\n", it, it_end - 1);
+  }
+#endif
   constexpr int C = klsh_ctx::kRing / 2;  // iterations per chunk
   uint64_t n_known = ctx->n_live;         // N after the last iteration the host has read
   const int h0 = floor_log2(n_known);

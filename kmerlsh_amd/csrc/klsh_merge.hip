@@ -50,7 +50,7 @@ constexpr bool kGramTiles = true;
 // Merge profiling (diagnostics build only: -DKLSH_MERGE_PROF, make prof): per size class, the
 // runs, rows, merges and wall-clock ticks (100 MHz) of each phase, summed over the call.
 #ifdef KLSH_MERGE_PROF
-__device__ unsigned long long g_mprof[8][8];
+__device__ unsigned long long g_mprof[8][12];  // [k] 8: loads, 9: norms, 10: walk loop
 #define MPROF_T() wall_clock64()
 #define MPROF_ADD(c, k, v) atomicAdd(&g_mprof[c][k], (unsigned long long)(v))
 #define MPROF_MAX(c, k, v) atomicMax(&g_mprof[c][k], (unsigned long long)(v))
@@ -59,7 +59,11 @@ __device__ unsigned long long g_sprof[8][8];  // small-run batches per G class: 
 __device__ unsigned long long g_wprof[8][8];  // walk phases in shader clocks: find, select+
                                               // consensus, dots, bits, steps, find rounds
 #define WPROF_CLK() __builtin_amdgcn_s_memtime()
+__device__ unsigned long long g_gprof[8];  // Gram tiles: tiles, ambiguous pairs, sum of the wave's
+                                           // longest lane list, clocks: acc, screen, exact, bits
+#define GPROF_ADD(k, v) atomicAdd(&g_gprof[k], (unsigned long long)(v))
 #else
+#define GPROF_ADD(k, v) (void)0
 #define MPROF_T() 0ull
 #define MPROF_ADD(c, k, v) (void)0
 #define MPROF_MAX(c, k, v) (void)0
@@ -82,6 +86,13 @@ __device__ __forceinline__ float shflf(float v, uint32_t src) { return __shfl(v,
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
   const uint32_t lo = shfl32((uint32_t)v, src), hi = shfl32((uint32_t)(v >> 32), src);
   return ((uint64_t)hi << 32) | lo;
+}
+// v_writelane_b32: lane `l` (a constant after unrolling) of v becomes the wave-uniform value s
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t s, int l) {
+  asm volatile("v_writelane_b32 %0, %1, %2"
+               : "=v"(v)
+               : "s"(__builtin_amdgcn_readfirstlane(s)), "i"(l), "0"(v));
+  return v;
 }
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
@@ -1420,6 +1431,110 @@ __device__ __forceinline__ void gram_decide(uint32_t R, uint32_t C, uint32_t b,
                                             const float* sq, const Decider& dc, uint64_t* P,
                                             int W, uint32_t* fb);
 
+template <int D, class RowA, class RowB>
+__device__ __forceinline__ void gram_decide_slow(uint32_t R, uint32_t C, uint32_t b,
+                                                 const f32x16 (&acc)[2][2], RowA rowA, RowB rowB,
+                                                 const float* sq, const Decider& dc, uint64_t* P,
+                                                 int W, uint32_t* fb);
+
+// The decisions from accumulated Gram values (gram_acc) as wave masks: every compare of the
+// 64 x 64 tile is one v_cmp whose lane mask IS the ballot the matrix words are assembled from, so
+// the screen has no branches, no per-pair LDS reads and no per-lane bit packing.  A pair is a hit
+// when G >= g_hi * den and a miss when G <= g_lo * den (den = sqrt|a|^2 * sqrt|b|^2, the
+// reference's, distance.cc:37; the products' rounding is ~1e-7 of a margin of 1e-4 -- a pair it
+// moves across g_hi or g_lo only changes between "settled" and "close call").  Rows past b enter
+// with sq = 1 and a zero Gram row/column (gram_acc's zero fill), so they are misses; the diagonal
+// tile masks c >= a.  A tile with any close call (or NaN, or a norm outside [2^-30, 2^30], where
+// den may leave the screen's range) goes to gram_decide_slow, which decides it exactly as before.
+// A tile without a hit writes nothing: P and fb start empty.
+template <int D, class RowA, class RowB>
+__device__ __forceinline__ void gram_decide(uint32_t R, uint32_t C, uint32_t b,
+                                            const f32x16 (&acc)[2][2], RowA rowA, RowB rowB,
+                                            const float* sq, const Decider& dc, uint64_t* P,
+                                            int W, uint32_t* fb) {
+  const uint32_t lane = __lane_id(), r = lane & 31u, h = lane >> 5;
+  const uint32_t a0 = R * 64u, c0 = C * 64u;
+  // the norms of my two columns and of my 32 rows (loaded together: one LDS wait)
+  float sc[2], sa[2][16];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const uint32_t c = c0 + 32u * n + r;
+    sc[n] = sq[min(c, b - 1u)];
+    sc[n] = c < b ? sc[n] : 1.0f;
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t a = a0 + 32u * m + (i & 3) + 8u * (i >> 2) + 4u * h;
+      sa[m][i] = sq[min(a, b - 1u)];
+      sa[m][i] = a < b ? sa[m][i] : 1.0f;
+    }
+  bool bad = false;
+  auto out = [](float v) { return !(v >= 0x1p-30f && v <= 0x1p30f); };
+#pragma unroll
+  for (int n = 0; n < 2; ++n) bad = bad || out(sc[n]);
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bad = bad || out(sa[m][i]);
+  const bool diag = R == C;
+  uint64_t anyhit = 0ull, close = __ballot(bad);
+  uint64_t own = 0ull;                       // lane L: the word of row a0 + L over the block's columns
+  uint32_t tm[2][2] = {{0u, 0u}, {0u, 0u}};  // column c0 + 32n + r: bits over rows 32m + .. (h = 0)
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float thi = dc.g_hi * sa[m][i], tlo = dc.g_lo * sa[m][i];
+      const uint32_t ar = (uint32_t)((i & 3) + 8 * (i >> 2));  // row within the half block (h = 0)
+      uint64_t bal[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const float g = acc[m][n][i];
+        uint64_t H = __ballot(g >= thi * sc[n]);
+        uint64_t L = __ballot(g <= tlo * sc[n]);
+        if (diag) {  // pairs c < a only (uniform branch)
+          const uint64_t lt = m < n ? 0ull : m > n ? ~0ull : __ballot(r < ar + 4u * h);
+          H &= lt;
+          L |= ~lt;
+        }
+        close |= ~(H | L);
+        anyhit |= H;
+        bal[n] = H;
+        tm[n][m] |= ((H >> lane) & 1ull) ? (1u << ar) : 0u;
+      }
+      // rows 32m + ar (lanes h = 0) and 32m + ar + 4 (h = 1): their words over the block's columns
+      const uint64_t w0 = (bal[0] & 0xFFFFFFFFull) | (bal[1] << 32);
+      const uint64_t w1 = (bal[0] >> 32) | (bal[1] & 0xFFFFFFFF00000000ull);
+      const int r0 = 32 * m + (int)ar;
+      uint32_t olo = (uint32_t)own, ohi = (uint32_t)(own >> 32);
+      olo = writelane(olo, (uint32_t)w0, r0);
+      ohi = writelane(ohi, (uint32_t)(w0 >> 32), r0);
+      olo = writelane(olo, (uint32_t)w1, r0 + 4);
+      ohi = writelane(ohi, (uint32_t)(w1 >> 32), r0 + 4);
+      own = ((uint64_t)ohi << 32) | olo;
+    }
+  if (close) {  // (wave-uniform) rare: the lane-by-lane path with the exact chains
+    gram_decide_slow<D>(R, C, b, acc, rowA, rowB, sq, dc, P, W, fb);
+    return;
+  }
+  if (!anyhit) return;
+  if (own && a0 + lane < b) {
+    atomicOr((unsigned long long*)&P[(a0 + lane) * W + C], (unsigned long long)own);
+    // fb (k_merge_long): row a's first match below it, over every column block
+    if (fb) atomicMin(&fb[a0 + lane], C * 64u + (uint32_t)__builtin_ctzll(own));
+  }
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    // my column's bits: rows 32m + ar + 4h of the block
+    const uint64_t mine = ((uint64_t)tm[n][1] << 32 | tm[n][0]) << (4u * h);
+    const uint64_t full = mine | shfl64(mine, lane ^ 32u);
+    const uint32_t c = c0 + 32u * n + r;
+    if (h == 0 && full && c < b) atomicOr((unsigned long long*)&P[c * W + R], (unsigned long long)full);
+  }
+}
+
 // One wave: the decisions of rows [R*64, R*64+64) against rows [C*64, C*64+64) (C <= R; pairs
 // c < a only), ORed into the position-space matrix P (W words per row, both P[a] bit c and
 // P[c] bit a).  rowA(a) / rowB(c) give the rows (LDS or memory); D = d, a multiple of 16.
@@ -1434,19 +1549,33 @@ __device__ __forceinline__ void gram_tile(uint32_t R, uint32_t C, uint32_t b, Ro
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.0f;
+  [[maybe_unused]] const uint64_t gc0 = WPROF_CLK();
   gram_acc<D>(R * 64u, C * 64u, b, rowA, rowB, acc);
+#ifdef KLSH_MERGE_PROF
+  asm volatile("s_nop 0" ::"v"(acc[1][1][15]) : "memory");
+  if (__lane_id() == 0) GPROF_ADD(3, WPROF_CLK() - gc0);
+#endif
+  [[maybe_unused]] const uint64_t gc1 = WPROF_CLK();
   gram_decide<D>(R, C, b, acc, rowA, rowB, sq, dc, P, W, fb);
+#ifdef KLSH_MERGE_PROF
+  if (__lane_id() == 0) {
+    GPROF_ADD(7, 1);
+    GPROF_ADD(4, WPROF_CLK() - gc1);
+  }
+#endif
 }
 
-// The decisions from accumulated Gram values (gram_acc): pre-screen against dc's margin, the
-// reference's sequential dot over D columns (rowA / rowB: whole rows) for the close calls.
+// The decisions from accumulated Gram values (gram_acc), lane by lane: pre-screen against dc's
+// margin, the reference's sequential dot over D columns (rowA / rowB: whole rows) for the close
+// calls.  gram_decide's path for a tile with a close call or a row of extreme norm.
 template <int D, class RowA, class RowB>
-__device__ __forceinline__ void gram_decide(uint32_t R, uint32_t C, uint32_t b,
-                                            const f32x16 (&acc)[2][2], RowA rowA, RowB rowB,
-                                            const float* sq, const Decider& dc, uint64_t* P,
-                                            int W, uint32_t* fb) {
+__device__ __forceinline__ void gram_decide_slow(uint32_t R, uint32_t C, uint32_t b,
+                                                 const f32x16 (&acc)[2][2], RowA rowA, RowB rowB,
+                                                 const float* sq, const Decider& dc, uint64_t* P,
+                                                 int W, uint32_t* fb) {
   const uint32_t lane = __lane_id(), r = lane & 31u, h = lane >> 5;
   const uint32_t a0 = R * 64u, c0 = C * 64u;
+  [[maybe_unused]] const uint64_t gcd = WPROF_CLK();
   // decisions: acc[m][n][i] is G[a][c] with a = a0 + 32m + (i&3) + 8(i>>2) + 4h, c = c0 + 32n + r;
   // bit e = 32m + 16n + i of hitm / ambm
   uint64_t hitm = 0ull, ambm = 0ull;
@@ -1465,6 +1594,22 @@ __device__ __forceinline__ void gram_decide(uint32_t R, uint32_t C, uint32_t b,
           ambm |= (uint64_t)(v >> 1) << e;
         }
       }
+#ifdef KLSH_MERGE_PROF
+  asm volatile("s_nop 0" ::"v"((uint32_t)ambm) : "memory");
+  [[maybe_unused]] uint64_t gc1 = WPROF_CLK();
+  {
+    const uint32_t na = (uint32_t)__builtin_popcountll(ambm);
+    uint32_t mx = na;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    uint32_t sm = na;
+    for (int o = 32; o > 0; o >>= 1) sm += (uint32_t)__shfl_xor((int)sm, o, 64);
+    if (lane == 0) {
+      GPROF_ADD(0, 1);
+      GPROF_ADD(1, sm);
+      GPROF_ADD(2, mx);
+    }
+  }
+#endif
   while (ambm) {  // rare: the exact sequential dot (the reference's order) decides
     const int e = __builtin_ctzll(ambm);
     ambm &= ambm - 1ull;
@@ -1484,6 +1629,14 @@ __device__ __forceinline__ void gram_decide(uint32_t R, uint32_t C, uint32_t b,
     }
     if (decide(dc, sdot, sq[a] * sq[c])) hitm |= 1ull << e;
   }
+#ifdef KLSH_MERGE_PROF
+  {
+    asm volatile("s_nop 0" ::"v"((uint32_t)hitm) : "memory");
+    const uint64_t gc2 = WPROF_CLK();
+    if (lane == 0) GPROF_ADD(5, gc2 - gc1);
+    gc1 = gc2;
+  }
+#endif
   uint64_t tmask[2] = {0ull, 0ull};  // column c0+32n+r: bits over the 64 rows of block R
   uint64_t own = 0ull;                // lane L ends up with the word of row a0 + L
 #pragma unroll
@@ -1801,6 +1954,7 @@ __device__ __forceinline__ void big_walk_reg(uint32_t p, uint32_t b, uint64_t* P
     if (lane == 0) wbuf[par * NW + wv] = best;
   };
   uint32_t size = b, par = 0;
+  [[maybe_unused]] const uint64_t wt0 = MPROF_T();
   {
     uint64_t hit[KP];
 #pragma unroll
@@ -1965,6 +2119,7 @@ __device__ __forceinline__ void big_walk_reg(uint32_t p, uint32_t b, uint64_t* P
     atomicAdd(&g_wprof[cls][4], (unsigned long long)steps);
     for (int k = 0; k < 4; ++k) atomicAdd(&g_wprof[cls][k], (unsigned long long)wp[k]);
     atomicAdd(&g_wprof[cls][5], (unsigned long long)wp[5]);
+    MPROF_ADD(RB <= 128 ? 0 : RB <= 192 ? 1 : RB <= 384 ? 2 : 3, 10, MPROF_T() - wt0);
   }
 #endif
   __syncthreads();
@@ -2064,6 +2219,9 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
             *reinterpret_cast<const float4*>(r.x + (size_t)slots[p + a] * r.dp + k);
       }
       __syncthreads();
+#ifdef KLSH_MERGE_PROF
+      if (t == 0) MPROF_ADD(cls, 8, MPROF_T() - pt0);
+#endif
       // norms recomputed from the rows in LDS (the cached chain, distance.cc:33-34: same bits)
       // instead of a random 4-B read each
       for (uint32_t a = t; a < b; a += NT) {
@@ -2081,6 +2239,9 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
       }
     }
     __syncthreads();
+#ifdef KLSH_MERGE_PROF
+    if (t == 0) MPROF_ADD(cls, 9, MPROF_T() - pt0);
+#endif
 
     // decisions in 64x64 tiles (row block R, column block C <= R): lanes = rows of R with the
     // row in registers, columns walked in order (LDS broadcast); the wave's ballot at column c
@@ -3856,7 +4017,7 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
 // Prints and clears the merge profile (diagnostics build only; a no-op otherwise).
 void merge_prof_dump(FILE* f) {
 #ifdef KLSH_MERGE_PROF
-  unsigned long long h[8][8];
+  unsigned long long h[8][12];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mprof), sizeof(h)) != hipSuccess) return;
   const char* names[kBigClasses + 1] = {"big128", "big192", "big384", "big896", "huge"};
   for (int c = 0; c <= kBigClasses; ++c)
@@ -3865,6 +4026,10 @@ void merge_prof_dump(FILE* f) {
                  "  (per run %7.2f + %7.2f us)  max run %8.2f us  max b %llu\n",
               names[c], h[c][0], h[c][1], h[c][2], h[c][3] * 1e-5, h[c][4] * 1e-5,
               h[c][3] * 1e-2 / h[c][0], h[c][4] * 1e-2 / h[c][0], h[c][5] * 1e-2, h[c][6]);
+  for (int c = 0; c <= kBigClasses; ++c)
+    if (h[c][0])
+      fprintf(f, "[mprof] %-7s per run: loads %7.2f  +norms %7.2f  (cum) us;  walk loop %7.2f us\n",
+              names[c], h[c][8] * 1e-2 / h[c][0], h[c][9] * 1e-2 / h[c][0], h[c][10] * 1e-2 / h[c][0]);
   unsigned long long wpf[8][8];
   if (hipMemcpyFromSymbol(wpf, HIP_SYMBOL(g_wprof), sizeof(wpf)) == hipSuccess)
     for (int c = 0; c < kBigClasses; ++c)
@@ -3881,10 +4046,17 @@ void merge_prof_dump(FILE* f) {
         fprintf(f, "[sprof] G=%-2d batches %9llu  clocks/batch: stage %7.0f  pairwise %7.0f  walk %7.0f"
                    "  write %7.0f\n", 2 << c, spf[c][0], (double)spf[c][1] / spf[c][0],
                 (double)spf[c][2] / spf[c][0], (double)spf[c][3] / spf[c][0], (double)spf[c][4] / spf[c][0]);
-  unsigned long long z[8][8] = {};
+  unsigned long long g[8];
+  if (hipMemcpyFromSymbol(g, HIP_SYMBOL(g_gprof), sizeof(g)) == hipSuccess && g[7])
+    fprintf(f, "[gprof] tiles %llu (gram_tile)  clocks/tile: acc %.0f  decide %.0f;  slow-path tiles %llu:"
+               " close pairs %llu (longest lane %.2f per slow tile), exact loop clocks/slow tile %.0f\n",
+            g[7], (double)g[3] / g[7], (double)g[4] / g[7], g[0], g[1], (double)g[2] / g[0],
+            (double)g[5] / g[0]);
+  unsigned long long z[8][12] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gprof), z, sizeof(g));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mprof), z, sizeof(z));
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), z, sizeof(z));
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sprof), z, sizeof(z));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), z, sizeof(unsigned long long) * 64);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sprof), z, sizeof(unsigned long long) * 64);
 #else
   (void)f;
 #endif
