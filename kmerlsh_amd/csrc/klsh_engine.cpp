@@ -588,7 +588,13 @@ static void count_class_rows(klsh_stats* st, const Counters& c, uint64_t n, bool
   st->kern[KC_HUGE].rows += c.n_huge_rows;
   st->kern[KC_HUGE].runs += c.n_huge;
   if (tail) {
-    st->kern[KC_TAIL].rows += c.n_small_rows + big_rows;
+    if (c.screened) {  // the screen saw every small run, k_merge_tail the ones it passed
+      st->kern[KC_SCREEN].rows += c.n_small_rows;
+      st->kern[KC_SCREEN].runs += small_runs;
+      st->kern[KC_TAIL].rows += c.n_act_rows + big_rows;
+    } else {
+      st->kern[KC_TAIL].rows += c.n_small_rows + big_rows;
+    }
     st->kern[KC_TAIL].runs += small_runs + big_runs;
     return;
   }
@@ -1849,6 +1855,12 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->mw.tail_max = (uint32_t)value;
     return 0;
   }
+  if (n == "tail_screen") {
+    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "tail_screen must be 0 or 1");
+    ctx->mw.tail_screen = (uint32_t)value;
+    return 0;
+  }
+  if (n == "tail_screen_grid") return grid(&ctx->mw.tail_screen_grid);
   if (n == "small_screen") {
     if (value != 0 && value != 1) return fail(KLSH_E_ARG, "small_screen must be 0 or 1");
     ctx->mw.small_screen = (uint32_t)value;
@@ -1882,6 +1894,8 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "small_screen_grid") *value = ctx->mw.screen_grid;
   else if (n == "tail_merge_rows") *value = klsh::tail_merge_max(ctx->mw);
   else if (n == "small_screen") *value = ctx->mw.small_screen;
+  else if (n == "tail_screen") *value = ctx->mw.tail_screen;
+  else if (n == "tail_screen_grid") *value = ctx->mw.tail_screen_grid;
   else if (n == "wide_image") *value = ctx->wide_image;
   else if (n == "long_runs") *value = ctx->mw.long_off == 1u ? 0 : ctx->mw.long_off == 0u ? 1 : ctx->mw.long_off;
   else if (n == "wide_projection") *value = ctx->pw.wide_h16;

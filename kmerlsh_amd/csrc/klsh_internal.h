@@ -165,6 +165,10 @@ struct MergeWork {
   // decide on the matrix cores; 0 = none
   uint32_t wide_gram = 32;
   uint32_t small_screen = 1;  // "small_screen": 1 = screen the small runs on the fp16 image first
+  // "tail_screen": 1 = the small-run screen also runs in front of k_merge_tail (iterations below
+  // tail_merge_rows), whose small-run waves then walk only the runs it passed
+  uint32_t tail_screen = 1;
+  uint32_t tail_screen_grid;  // "tail_screen_grid": its persistent launch there (0: 2048)
   // "tail_merge_rows": below this many positions every merge class runs in ONE launch
   // (k_merge_tail); 0 = the default 2^20 (tests lower it to reach the per-class launches)
   uint32_t tail_max;

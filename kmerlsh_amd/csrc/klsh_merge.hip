@@ -1902,7 +1902,8 @@ __device__ __forceinline__ void big_walk(uint32_t p, uint32_t b, uint64_t* P, ui
 //    tested again — so it is computed once per rewritten row at the write-back.
 template <int RB, int NT, int D>
 __device__ __forceinline__ void big_walk_reg(uint32_t p, uint32_t b, uint64_t* P, uint32_t* slot,
-                                             float* nrm, uint32_t* cnt, uint32_t* hd, uint32_t* tl,
+                                             float* nrm, uint32_t* cnt, const uint32_t* cnt0,
+                                             uint32_t* hd, uint32_t* tl,
                                              uint32_t* pos2row, float* sq, float* rowsL,
                                              float* cwall, uint64_t* wbuf, const Rows& r,
                                              const Decider& dc, uint32_t* slots, uint32_t* dlist,
@@ -2123,33 +2124,32 @@ __device__ __forceinline__ void big_walk_reg(uint32_t p, uint32_t b, uint64_t* P
   }
 #endif
   __syncthreads();
+  if (size == b) return;  // (block-uniform) no merge: the run, its rows and metadata are as loaded
   // write back: survivors in position order, kInvalid after; rewritten rows; metadata
   for (uint32_t q = t; q < b; q += NT) slots[p + q] = q < size ? slot[pos2row[q]] : kInvalid;
-  {  // a survivor was rewritten iff its count rose (the global count is still old)
+  {  // a survivor was rewritten iff its count rose
     constexpr uint32_t c4 = (uint32_t)D / 4;
     for (uint32_t idx = t; idx < size * c4; idx += NT) {
       const uint32_t q = idx / c4, k = (idx % c4) * 4;
       const uint32_t y = pos2row[q];
-      if (r.cnt[slot[y]] != cnt[y])
+      if (cnt0[y] != cnt[y])
         store_row4(r, (size_t)slot[y] * r.dp + k, *reinterpret_cast<const float4*>(rowsL + y * ST + k));
     }
-    __syncthreads();
   }
   for (uint32_t q0 = 0; q0 < size; q0 += NT) {  // uniform trip count (ballot inside)
     const uint32_t q = q0 + t;
     bool rewritten = false;
     if (q < size) {
       const uint32_t y = pos2row[q];
-      rewritten = r.cnt[slot[y]] != cnt[y];  // every merge into a row raises its count
-      float nv = nrm[y];
+      rewritten = cnt0[y] != cnt[y];  // every merge into a row raises its count
       if (rewritten) {  // the exact sequential norm of the new row (distance.cc:33-34)
-        nv = 0.0f;
+        float nv = 0.0f;
 #pragma unroll
         for (int k = 0; k < D; ++k) nv = nv + rowsL[y * ST + k] * rowsL[y * ST + k];
+        r.nrm[slot[y]] = nv;
+        r.cnt[slot[y]] = cnt[y];
+        r.head[slot[y]] = hd[y];
       }
-      r.nrm[slot[y]] = nv;
-      r.cnt[slot[y]] = cnt[y];
-      r.head[slot[y]] = hd[y];
     }
     if (dlist) append_slot(rewritten, q < size ? slot[pos2row[q]] : 0u, dlist, &ctr->n_delta);
   }
@@ -2162,7 +2162,7 @@ struct BigLayout {
   static constexpr size_t rows = 0;
   static constexpr size_t P = rows + sizeof(float) * ST * (ROWS_LDS ? RB : 64);
   static constexpr size_t meta = P + sizeof(uint64_t) * RB * W;
-  static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 7;
+  static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 8;
 };
 
 // The runs li = first, first + stride, ... (< count) of list `list` (size class cls), one
@@ -2184,6 +2184,7 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
   uint32_t* tl = slot + 4 * RB;
   uint32_t* pos2row = slot + 5 * RB;
   float* sq = reinterpret_cast<float*>(slot + 6 * RB);  // sqrtf(nrm), distance.cc:37
+  uint32_t* cnt0 = slot + 7 * RB;                       // the counts as loaded (rewritten rows)
   __shared__ uint32_t wbuf[2 * NW];
   __shared__ __attribute__((aligned(16))) float cwall[NW * 64];  // big_walk_reg's new-row copies
   __shared__ uint64_t wbuf64[2 * NW];                              // big_walk_reg's published hits
@@ -2197,28 +2198,71 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
     const uint32_t p = e.x, b = e.y;
     const uint32_t nblk = (b + 63) / 64;
     [[maybe_unused]] const uint64_t pt0 = MPROF_T();
-    for (uint32_t a = t; a < b; a += NT) {
-      const uint32_t s = slots[p + a];
-      slot[a] = s;
-      if constexpr (!ROWS_LDS) {
+    if constexpr (!ROWS_LDS) {
+      for (uint32_t a = t; a < b; a += NT) {
+        const uint32_t s = slots[p + a];
+        slot[a] = s;
         nrm[a] = r.nrm[s];
         sq[a] = __builtin_sqrtf(nrm[a]);
+        cnt[a] = cnt0[a] = r.cnt[s];
+        hd[a] = r.head[s];
+        tl[a] = r.tail[s];
+        pos2row[a] = a;
       }
-      cnt[a] = r.cnt[s];
-      hd[a] = r.head[s];
-      tl[a] = r.tail[s];
-      pos2row[a] = a;
     }
     for (uint32_t a = t; a < b * (uint32_t)W; a += NT) P[a] = 0ull;
     if constexpr (ROWS_LDS) {
-      // the rows in the same round of loads as the metadata (each lane reads its row's slot
-      // itself: no barrier, and so no second memory latency, between the two)
-      for (uint32_t q = t; q < b * (uint32_t)(D / 4); q += NT) {
-        const uint32_t a = q / (D / 4), k = (q % (D / 4)) * 4;
-        *reinterpret_cast<float4*>(rows + a * ST + k) =
-            *reinterpret_cast<const float4*>(r.x + (size_t)slots[p + a] * r.dp + k);
+      // Three memory latencies, every load of a round in flight at once (loads under a bounds
+      // branch would each be waited for on the spot): the run's slots; then the metadata and
+      // the rows by slot, d/4 lanes per row, a float4 each, KB rows per lane per round.
+      constexpr int KA = (RB + NT - 1) / NT;
+      uint32_t sl[KA], mc[KA], mh[KA], mt[KA];
+#pragma unroll
+      for (int ka = 0; ka < KA; ++ka) sl[ka] = slots[p + min(t + (uint32_t)ka * NT, b - 1u)];
+#pragma unroll
+      for (int ka = 0; ka < KA; ++ka) {
+        mc[ka] = r.cnt[sl[ka]];
+        mh[ka] = r.head[sl[ka]];
+        mt[ka] = r.tail[sl[ka]];
       }
-      __syncthreads();
+#pragma unroll
+      for (int ka = 0; ka < KA; ++ka) {
+        const uint32_t a = t + (uint32_t)ka * NT;
+        if (a < b) {
+          slot[a] = sl[ka];
+          pos2row[a] = a;
+        }
+      }
+      lds_barrier();  // slot[] (the metadata loads stay in flight)
+      constexpr uint32_t LPR = (uint32_t)D / 4;  // lanes per row: a float4 each
+      constexpr uint32_t RPR = NT / LPR;         // rows per workgroup round
+      constexpr int KB = D >= 64 ? 8 : D >= 32 ? 4 : 2;
+      static_assert(D % 4 == 0 && NT % LPR == 0, "whole rows per round");
+      const uint32_t sub = (t % LPR) * 4u, rr = t / LPR;
+      const uint32_t rounds = (b + RPR - 1u) / RPR;
+      for (uint32_t g0 = 0; g0 < rounds; g0 += KB) {  // block-uniform
+        float4 v[KB];
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const uint32_t a = min((g0 + (uint32_t)k) * RPR + rr, b - 1u);
+          v[k] = *reinterpret_cast<const float4*>(r.x + (size_t)slot[a] * r.dp + sub);
+        }
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+          const uint32_t a = (g0 + (uint32_t)k) * RPR + rr;
+          if (a < b) *reinterpret_cast<float4*>(rows + a * ST + sub) = v[k];
+        }
+      }
+#pragma unroll
+      for (int ka = 0; ka < KA; ++ka) {
+        const uint32_t a = t + (uint32_t)ka * NT;
+        if (a < b) {
+          cnt[a] = cnt0[a] = mc[ka];
+          hd[a] = mh[ka];
+          tl[a] = mt[ka];
+        }
+      }
+      lds_barrier();
 #ifdef KLSH_MERGE_PROF
       if (t == 0) MPROF_ADD(cls, 8, MPROF_T() - pt0);
 #endif
@@ -2317,8 +2361,8 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
     __syncthreads();
     [[maybe_unused]] const uint64_t pt1 = MPROF_T();
     if constexpr (ROWS_LDS && D > 0 && D <= 64) {
-      big_walk_reg<RB, NT, D>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq, rows, cwall, wbuf64, r,
-                              dc, slots, dlist, ctr);
+      big_walk_reg<RB, NT, D>(p, b, P, slot, nrm, cnt, cnt0, hd, tl, pos2row, sq, rows, cwall,
+                              wbuf64, r, dc, slots, dlist, ctr);
     } else {
       big_walk<RB, NT, ROWS_LDS, D>(p, b, P, slot, nrm, cnt, hd, tl, pos2row, sq,
                                  ROWS_LDS ? rows : nullptr, ST, rows, wbuf, r, dc, slots, dlist,
@@ -3553,7 +3597,7 @@ struct BigWideLayout {
   static constexpr size_t tiles = 0;
   static constexpr size_t P = tiles + sizeof(float) * NW * 64 * STB;
   static constexpr size_t meta = P + sizeof(uint64_t) * RB * W;
-  static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 7;
+  static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 8;
 };
 
 template <int RB, int NT, int KC>
@@ -3823,7 +3867,19 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
     // 1024 swept (round 3)
     const uint32_t nbig = w.tail_nbig ? w.tail_nbig : 128u;
     const uint32_t nsmall = w.tail_nsmall ? w.tail_nsmall : 512u;
-    k_merge_tail<D><<<nbig + nsmall, 256, lds, s>>>(w, slots, dc, r, ctr, nbig);
+    MergeWork wt = w;
+    if (w.tail_screen && screen_ok(r, dc, w)) {
+      // the fp16 screen of the small runs first (few of them merge this late in the loop), on
+      // the same stream: k_merge_tail's small-run waves then take only the runs it passed
+      float m0, a2;
+      screen_margins(r.d, &m0, &a2);
+      // (option tail_screen_grid; one box, interleaved C2: 512 → 214.9, 1024 → 210.0, 2048 →
+      // 208.1 ms per step; tail_screen = 0: 213.3 ms)
+      const uint32_t sgrid = w.tail_screen_grid ? std::max(64u, w.tail_screen_grid) : 2048u;
+      k_small_screen<D><<<sgrid, 64, 0, s>>>(w, slots, r, dc.s_star, m0, a2, w.kt);
+      wt.screened = 1u;
+    }
+    k_merge_tail<D><<<nbig + nsmall, 256, lds, s>>>(wt, slots, dc, r, ctr, nbig);
     return;
   }
   const Fork f(w, s);
