@@ -624,7 +624,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
   constexpr int NR = kScreenAhead + 1;            // row buffers: the screened batch + the ones ahead
   constexpr uint32_t kBuf = 256;                  // passed runs kept in LDS before a flush
   __shared__ __attribute__((aligned(16))) _Float16 lrow[64 * STH];
-  __shared__ float linv[64];
+  __shared__ __attribute__((aligned(16))) float linv[64];
   __shared__ uint32_t lflag[64];  // per run of the batch: some pair not ruled out
   __shared__ uint2 buf[kBuf];     // passed runs (start, length | class << 16)
   __shared__ uint32_t fcnt[NC], fbase[NC];
@@ -735,14 +735,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
     // The Gram blocks of the batch's runs on the matrix cores (x~ . x~ exact products, f32 sums):
     // 32 x 32 tiles for runs of 17..64 rows (the upper-triangular tiles of each run), 16 x 16
     // diagonal tiles for shorter runs (4 per batch, runs never cross a 16-row block).  A pair
-    // (R < C) of one run that the screen cannot rule out flags the run in LDS.
-    auto test = [&](uint32_t R, uint32_t C, float sv) {
-      if (R < C && (R >> lg) == (C >> lg) && ((vmask >> R) & (vmask >> C) & 1ull)) {
-        const float ir = linv[R], ic = linv[C];
-        const float qv = sv * ir * ic;
-        const float m = m0 + a2 * (ir + ic);
-        if (!(qv < s_star - m)) lflag[R >> lg] = 1u;  // NaN / inf: not ruled out
-      }
+    // (R < C) of one run that the screen cannot rule out flags the run in LDS.  The tests of a
+    // lane's tile entries are branch-free over inverse norms loaded up front (a load inside each
+    // test's branch was a wait on LDS per entry); the flag store is the only predicated step.
+    auto test = [&](uint32_t R, uint32_t C, float sv, float ir, float ic) -> bool {
+      const bool pair = (R < C) & ((R >> lg) == (C >> lg)) & (((vmask >> R) & (vmask >> C) & 1ull) != 0ull);
+      const float qv = sv * ir * ic;
+      const float m = m0 + a2 * (ir + ic);
+      return pair & !(qv < s_star - m);  // NaN / inf: not ruled out
     };
     if constexpr (D < 32) {  // (not launched: screen_ok needs d >= 32) rule nothing out
       lflag[lane] = 1u;
@@ -761,10 +761,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
           const sh16x8 fb = *reinterpret_cast<const sh16x8*>(lrow + (tc * 32u + r32) * STH + 16 * ks + k8);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
         }
+        const uint32_t C = tc * 32u + r32;
+        const float ic = linv[C];
+        float4 irv[4];  // rows tr*32 + 8j + 4h + (0..3)
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-          test(tr * 32u + (uint32_t)(q & 3) + 8u * (uint32_t)(q >> 2) + 4u * (lane >> 5),
-               tc * 32u + r32, acc[q]);
+        for (int j = 0; j < 4; ++j)
+          irv[j] = *reinterpret_cast<const float4*>(linv + tr * 32u + 8u * (uint32_t)j + 4u * (lane >> 5));
+        bool fail = false;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const float4 v = irv[q >> 2];
+          const float ir = (q & 3) == 0 ? v.x : (q & 3) == 1 ? v.y : (q & 3) == 2 ? v.z : v.w;
+          fail |= test(tr * 32u + (uint32_t)(q & 3) + 8u * (uint32_t)(q >> 2) + 4u * (lane >> 5), C,
+                       acc[q], ir, ic);
+        }
+        if (fail) lflag[C >> lg] = 1u;
       }
     } else {
       const uint32_t r16 = lane & 15u, k8 = 8u * (lane >> 4);
@@ -776,9 +787,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
           const sh16x8 f = *reinterpret_cast<const sh16x8*>(lrow + (16u * tb + r16) * STH + 32 * ks + k8);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(f, f, acc, 0, 0, 0);
         }
+        const uint32_t C = 16u * tb + r16;
+        const float ic = linv[C];
+        const float4 v = *reinterpret_cast<const float4*>(linv + 16u * tb + 4u * (lane >> 4));
+        const float irq[4] = {v.x, v.y, v.z, v.w};
+        bool fail = false;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          test(16u * tb + 4u * (lane >> 4) + (uint32_t)q, 16u * tb + r16, acc[q]);
+          fail |= test(16u * tb + 4u * (lane >> 4) + (uint32_t)q, C, acc[q], irq[q], ic);
+        if (fail) lflag[C >> lg] = 1u;
       }
     }
     wave_lds_fence();
