@@ -16,7 +16,7 @@ scaling, value = N_0 * I / T of the one job.  --mode replicas instead runs an in
 per rank (seed 11 + rank, no collective; weak scaling).  Barrier + max-over-ranks timing.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c4|c5]
-                    [--mode sharded|replicas] [--cpu-baseline auto|reference|port|none]
+                    [--mode sharded|replicas] [--cpu-baseline auto|reference|port|full|none]
 """
 from __future__ import annotations
 
@@ -140,50 +140,90 @@ def state_at(eng, t, min_sim, iters, counter0):
     return eng.result()
 
 
+def schedule_threshold(min_sim, iters, t):
+    """Cluster()'s threshold at iteration t (function/cluster.cc:190-192,330), in float32 as the
+    reference computes it: 0.95f, then -= sim_step per iteration."""
+    thr = np.float32(0.95)
+    step = np.float32((np.float32(0.95) - np.float32(min_sim)) / np.float32(iters))
+    for _ in range(t):
+        thr = np.float32(thr - step)
+    return float(thr)
+
+
+def write_state(tmp, rows, off, ids):
+    src = os.path.join(tmp, "rows.f32")
+    rows.astype("<f4").tofile(src)
+    off.astype("<u8").tofile(src + ".off")
+    ids.astype("<u8").tofile(src + ".ids")
+    return src
+
+
 def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
-    """The reference (oracle/_ref/ref_harness: the reference's own Cluster(), compiled from its
-    sources) or the oracle port, timed on this host's cores over a bounded sample of the same
-    loop: one iteration from the loop's own state at t = 0, .1 I, .2 I, .4 I, .6 I, .9 I (the
-    engine provides the state).  Its per-row cost, interpolated in t and weighted by the loop's
-    N_t trace, estimates T_loop; value = N_0 * I / T_loop like the metric.  The sampled iteration
-    runs at the reference's first-iteration threshold 0.95 (Cluster() always starts there), not
-    at the schedule's value at t: fewer merges, so the estimate favours the CPU slightly."""
+    """The reference (oracle/_ref/ref_harness: the reference's own functions, compiled from its
+    sources) or the oracle port, timed on this host's cores.
+
+    Default (a bounded sample): one iteration of the loop from its own state at t = 0, .1 I, .2 I,
+    .4 I, .6 I, .9 I (the engine provides the state) at the schedule's threshold for t — the
+    harness's iter_w, Cluster()'s loop body through the reference's p_lsh, merge_hashtable,
+    p_cluster / nestedCluster and merge_abundance (Cluster() itself would start at 0.95).  Its
+    per-row cost, interpolated in t and weighted by the loop's N_t trace, estimates T_loop; value
+    = N_0 * I / T_loop like the metric.  mode "full": the reference's WHOLE main loop timed once
+    (its own Cluster() over all I iterations from the post-init state, ~5 min at C2 on 16
+    threads), with the sampled estimate beside it."""
     if mode == "none":
         return None
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     threads = min(16, os.cpu_count() or 1)
     kind = None
-    if mode in ("auto", "reference") and os.path.exists(harness):
+    if mode in ("auto", "reference", "full") and os.path.exists(harness):
         kind = "reference"
     elif mode in ("auto", "port"):
         kind = "port"
     if kind is None:
         return None
+    env = dict(os.environ, OMP_THREAD_LIMIT=str(threads), OMP_NUM_THREADS=str(threads),
+               KLSH_REF_THREADS=str(threads), KLSH_SEED=str(SEED_BASE))
+    full = None
+    if mode == "full" and kind == "reference":
+        rows, off, ids = state_at(eng, 0, min_sim, iters, counter0)
+        n_t = rows.shape[0]
+        with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
+            src = write_state(tmp, rows, off, ids)
+            del rows, off, ids
+            log(f"cpu baseline: the reference's whole loop, {iters} iterations from {n_t} rows, "
+                f"{threads} threads")
+            out = subprocess.run([harness, "cluster_w", src, src + ".off", src + ".ids", str(n_t),
+                                  str(d), repr(float(min_sim)), str(iters), "1000000",
+                                  os.path.join(tmp, "out")], env=env, check=True,
+                                 capture_output=True, text=True, timeout=3000).stdout
+        secs = float(re.findall(r"hash\+cluster takes \(secs\): ([0-9.eE+-]+)", out)[-1])
+        sizes = [int(v) for v in re.findall(r"Size of profilings\D*(\d+)", out)]
+        log(f"cpu baseline: reference loop {secs:.1f} s")
+        # (at T > 1 the reference's concatenation order depends on OpenMP scheduling,
+        # cluster.cc:281, so its N_t trace is its own, not the T = 1 trace the engine matches)
+        full = {"value": n0 * iters / secs, "loop_s": secs, "sum_trace": int(sum(sizes[-iters:])),
+                "final_rows": int(re.findall(r"after clustering:\s*(\d+)", out)[-1])}
     trace = np.asarray(trace, dtype=np.float64)
     ts = sorted({min(iters - 1, int(f * iters)) for f in (0.0, 0.1, 0.2, 0.4, 0.6, 0.9)})
     cost, secs_all = [], 0.0
     for t in ts:
         rows, off, ids = state_at(eng, t, min_sim, iters, counter0)
         n_t = rows.shape[0]
+        thr_t = schedule_threshold(min_sim, iters, t)
         if kind == "reference":
             with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
-                src = os.path.join(tmp, "rows.f32")
-                rows.astype("<f4").tofile(src)
-                off.astype("<u8").tofile(src + ".off")
-                ids.astype("<u8").tofile(src + ".ids")
+                src = write_state(tmp, rows, off, ids)
                 del rows, off, ids
-                env = dict(os.environ, OMP_THREAD_LIMIT=str(threads), OMP_NUM_THREADS=str(threads),
-                           KLSH_REF_THREADS=str(threads), KLSH_SEED=str(SEED_BASE))
-                out = subprocess.run([harness, "cluster_w", src, src + ".off", src + ".ids",
-                                      str(n_t), str(d), repr(float(min_sim)), "1", "1000000",
-                                      os.path.join(tmp, "out")], env=env, check=True,
-                                     capture_output=True, text=True, timeout=900).stdout
-            secs = float(re.findall(r"hash\+cluster takes \(secs\): ([0-9.eE+-]+)", out)[-1])
+                out = subprocess.run([harness, "iter_w", src, src + ".off", src + ".ids",
+                                      str(n_t), str(d), repr(thr_t), "1000000"], env=env,
+                                     check=True, capture_output=True, text=True,
+                                     timeout=900).stdout
+            secs = float(re.findall(r"one iteration takes \(secs\): ([0-9.eE+-]+)", out)[-1])
         else:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import klsh_oracle
 
-            t0 = time.perf_counter()
+            t0 = time.perf_counter()  # (the oracle's one-iteration call runs at 0.95)
             klsh_oracle.cluster(rows, float(min_sim), 1, 1_000_000, SEED_BASE, 0, off, ids, threads)
             secs = time.perf_counter() - t0
         log(f"cpu baseline ({kind}, {threads} threads): t={t} N_t={n_t}: {secs:.2f} s")
@@ -192,13 +232,26 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
     per_row = np.interp(np.arange(len(trace)), ts, cost)
     t_loop = float((trace * per_row).sum())
     c1 = c1_measured(harness, threads) if kind == "reference" else None
-    return {"value": n0 * iters / t_loop, "unit": "k-mers·iterations/s", "cores": threads,
-            "c1_measured": c1,
-            "kind": kind, "estimated_loop_s": round(t_loop, 2), "sample_seconds": round(secs_all, 2),
-            "sample": (f"one iteration of the main loop from its own state at t = "
-                       f"{', '.join(map(str, ts))} of {iters} ({threads} threads, threshold 0.95); "
-                       f"per-row cost interpolated in t and weighted by the loop's N_t trace "
-                       f"(sum N_t = {int(trace.sum())}) to estimate T_loop")}
+    sampled = {"value": n0 * iters / t_loop, "estimated_loop_s": round(t_loop, 2),
+               "sample_seconds": round(secs_all, 2),
+               "sample": (f"one iteration of the main loop from its own state at t = "
+                          f"{', '.join(map(str, ts))} of {iters} ({threads} threads, at the "
+                          f"schedule's threshold for t"
+                          + (", reference harness iter_w" if kind == "reference" else
+                             "; the port's one-iteration call runs at 0.95") +
+                          f"); per-row cost interpolated in t and weighted by the loop's N_t "
+                          f"trace (sum N_t = {int(trace.sum())}) to estimate T_loop")}
+    if full:
+        return {"value": full["value"], "unit": "k-mers·iterations/s", "cores": threads,
+                "kind": "reference_full", "loop_s": round(full["loop_s"], 2),
+                "reference_sum_trace": full["sum_trace"], "reference_final_rows": full["final_rows"],
+                "sample": (f"the reference's whole main loop ({iters} iterations, its own Cluster()"
+                           f" through oracle/_ref/ref_harness cluster_w) from the post-init state, "
+                           f"{threads} threads, timed once"),
+                "sampled_estimate": dict(sampled, ratio_to_full=round(t_loop / full["loop_s"], 4)),
+                "c1_measured": c1}
+    return dict({"unit": "k-mers·iterations/s", "cores": threads, "kind": kind, "c1_measured": c1},
+                **sampled)
 
 
 def c1_measured(harness, threads):
@@ -306,15 +359,15 @@ BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 def kernel_rooflines(config, stats, steps, d, trace, shadow):
     """Every kernel class's achieved HBM rate (its algorithmic bytes per launch over its average
     HIP-event launch time); the headline is the class with the largest time per step."""
-    import math
-
     register = d in (8, 16, 32, 64)
-    # shadow: the projection reads the fp16 row image (2d bytes a row; the engine keeps one at
-    # d = 16, 32, 64 and d > 64 with d % 8 == 0 unless option "projection" = 1 / "wide_image" = 0);
-    # its close calls re-read the f32 row
-    row_bytes = 2 * d if shadow else 4 * d
+    # SURVEY.md 8(d) bytes: the projection reads the f32 row (4d), a slot and writes a key.
+    # shadow: what it actually reads is the fp16 row image (2d bytes a row; the engine keeps one at
+    # d = 16, 32, 64 and d > 64 with d % 8 == 0 unless option "projection" = 1 / "wide_image" = 0),
+    # plus the f32 row of the close calls: reported beside it as "image"
+    row_bytes = 4 * d
     kern = {c: {f: sum(s["kern"][c][f] for s in stats) for f in ("ms", "launches", "rows", "runs")}
             for c in stats[0]["kern"]}
+    merge_phase = kern.pop("merge", None)
     merges_small = sum(s["small_iter_merges"] for s in stats)
     tr = np.asarray(trace, dtype=np.float64)
     tr = tr[tr > 1]
@@ -369,6 +422,12 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
         if c == "project":
             bits = sum(s["sum_proj_bits"] for s in stats)
             if shadow:
+                ib = rows * (2 * d + 8) / k["launches"]
+                ia = ib / (e["avg_launch_ms"] * 1e-3) / 1e9
+                e["image"] = {"bytes_per_launch": ib, "achieved": round(ia, 2),
+                              "frac": round(ia / HBM_PEAK_GBS, 5),
+                              "note": "the bytes the kernel must read: the fp16 row image "
+                                      "(2d) + slot + key per row, same launch time"}
                 # the fp16-image screen: S = X~ (w_hi + w_lo)^T, 2 f16 MFMA products per product
                 # (wide rows: a third, |x~|.|w_hi|, for the bound)
                 fl = (2 if register else 3) * 2.0 * bits * d / k["launches"]
@@ -418,6 +477,28 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
     alone = [e for e in out if not e.get("overlapped")] or out
     head = dict(max(alone, key=lambda e: e["ms_per_step"]))
     head["kernels"] = sorted(out, key=lambda e: -e["ms_per_step"])
+    # The merge PHASE of the iterations whose classes run as separate concurrent launches
+    # (N_t >= 2^20 at the register widths, every iteration at d > 64): first workgroup start of any
+    # merge class to the last end, per iteration (KLSH_K_MERGE stamps), against SURVEY.md 8(d)'s
+    # merge share of B_t: N_t x 4d (every row read for the in-bucket merge) + M_t x (4d + 8) (the
+    # new row and a member link per merge), summed over those iterations.
+    if merge_phase and merge_phase["launches"]:
+        tr = np.asarray(trace, dtype=np.float64)
+        nxt = np.append(tr[1:], float(stats[-1]["n_final"]))
+        sel = tr >= (1 << 20) if register else tr >= 0
+        mb = float((tr[sel] * 4 * d + (tr[sel] - nxt[sel]) * (4 * d + 8)).sum())
+        ms = merge_phase["ms"] / steps
+        n_it = merge_phase["launches"] / steps
+        ach = mb / (ms * 1e-3) / 1e9
+        head["phases"] = [{
+            "phase": "merge wall of the multi-launch iterations" + (" (N_t >= 2^20)" if register else ""),
+            "iterations_per_step": n_it, "ms_per_step": ms, "bytes_per_step": mb,
+            "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 5),
+            "note": "KLSH_K_MERGE stamps: per iteration, the first merge-class workgroup start to "
+                    "the last end (the concurrent small-run screen, small-run merge and big-run "
+                    "classes together); bytes SURVEY.md 8(d): N_t*4d + M_t*(4d+8) over those "
+                    "iterations of the last step's trace"}]
     head["note"] = ("roofline = the kernel class with the largest time per step among the launches "
                     "that run alone (the concurrent merge classes are marked overlapped: their spans "
                     "include waits for CUs behind each other); a launch's time "
@@ -434,7 +515,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "none"])
+    ap.add_argument("--cpu-baseline", default="auto",
+                    choices=["auto", "reference", "port", "full", "none"],
+                    help="full: the reference's whole main loop timed once (C2: minutes)")
     ap.add_argument("--mode", default="sharded", choices=["sharded", "replicas"],
                     help="N>1: one problem sharded over the ranks (C3) or one problem per rank")
     ap.add_argument("--phases", action="store_true",

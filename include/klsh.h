@@ -39,8 +39,9 @@ extern "C" {
 
 /* ABI version of this header.  2: every statistics struct starts with `struct_size`, which the
  * caller sets to sizeof(the struct) (the library refuses a mismatch instead of writing past a
- * smaller struct); klsh_stats.kern has KLSH_KCLASSES = 12 classes; klsh_get_option. */
-#define KLSH_ABI_VERSION 2
+ * smaller struct); klsh_get_option.  3: klsh_stats.kern has KLSH_KCLASSES = 13 classes (the
+ * merge-phase wall, KLSH_K_MERGE). */
+#define KLSH_ABI_VERSION 3
 
 typedef struct klsh_ctx klsh_ctx;
 
@@ -60,7 +61,10 @@ typedef struct klsh_ctx klsh_ctx;
 #define KLSH_K_TAIL 9     /* iterations below 2^20 positions: every merge class in one k_merge_tail */
 #define KLSH_K_COMPACT 10 /* survivor compaction (span) */
 #define KLSH_K_SCREEN 11  /* fp16 screen of the runs of 2..64 rows (SMALL then merges the ones left) */
-#define KLSH_KCLASSES 12
+#define KLSH_K_MERGE 12   /* a phase, not a kernel: the merge launches of each iteration at >= 2^20
+                             positions (every iteration at d > 64) together — first workgroup start
+                             of any merge class to the last end (their concurrent wall) */
+#define KLSH_KCLASSES 13
 typedef struct klsh_kstat {
   double ms;
   uint64_t launches;

@@ -41,11 +41,11 @@ EXPORTED = (
 
 
 # include/klsh.h KLSH_ABI_VERSION (the structs below mirror that header)
-ABI_VERSION = 2
-# klsh_stats.kern indices (include/klsh.h KLSH_K_*)
+ABI_VERSION = 3
+# klsh_stats.kern indices (include/klsh.h KLSH_K_*); "merge" is a phase (KLSH_K_MERGE)
 KERNEL_CLASSES = ("project", "sort", "runs", "small", "big128", "big192", "big384", "big896",
-                  "huge", "tail", "compact", "screen")
-KCLASSES = 12
+                  "huge", "tail", "compact", "screen", "merge")
+KCLASSES = 13
 
 
 class KlshKstat(ctypes.Structure):
@@ -207,9 +207,17 @@ def load_library() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if not os.environ.get("KLSH_LIB") and lib.klsh_abi_version() != ABI_VERSION:
-        raise KlshError(f"{LIB_PATH}: ABI version {lib.klsh_abi_version()}, this binding "
-                        f"mirrors {ABI_VERSION}: rebuild the library")
+    # every library is checked, the KLSH_LIB ones (diagnostics / A/B builds, the likeliest to be
+    # stale) too; KLSH_ABI_ANY=1 turns the refusal into a warning for an older A/B build, whose
+    # calls with statistics structs then fail on their struct_size check instead
+    if hasattr(lib, "klsh_abi_version") and lib.klsh_abi_version() != ABI_VERSION:
+        msg = (f"{os.environ.get('KLSH_LIB') or LIB_PATH}: ABI version {lib.klsh_abi_version()}, "
+               f"this binding mirrors {ABI_VERSION}: rebuild the library")
+        if os.environ.get("KLSH_ABI_ANY") != "1":
+            raise KlshError(msg)
+        import warnings
+
+        warnings.warn(msg)
     _lib = lib
     return lib
 

@@ -10,12 +10,18 @@ namespace klsh {
 __device__ __forceinline__ unsigned long long stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
 // the workgroup's start / end (thread 0; its waves end within a few microseconds of each other)
 __device__ __forceinline__ void kt_begin(const KTime& kt, int c) {
-  if (kt.blk && threadIdx.x == 0)
-    atomicMin(&kt.blk->set[kt.set].t0[c][blockIdx.x % kStampSlots].v, stamp_now());
+  if (kt.blk && threadIdx.x == 0) {
+    const unsigned long long now = stamp_now();
+    atomicMin(&kt.blk->set[kt.set].t0[c][blockIdx.x % kStampSlots].v, now);
+    if (kt.phase >= 0) atomicMin(&kt.blk->set[kt.set].t0[kt.phase][blockIdx.x % kStampSlots].v, now);
+  }
 }
 __device__ __forceinline__ void kt_end(const KTime& kt, int c) {
-  if (kt.blk && threadIdx.x == 0)
-    atomicMax(&kt.blk->set[kt.set].t1[c][blockIdx.x % kStampSlots].v, stamp_now());
+  if (kt.blk && threadIdx.x == 0) {
+    const unsigned long long now = stamp_now();
+    atomicMax(&kt.blk->set[kt.set].t1[c][blockIdx.x % kStampSlots].v, now);
+    if (kt.phase >= 0) atomicMax(&kt.blk->set[kt.set].t1[kt.phase][blockIdx.x % kStampSlots].v, now);
+  }
 }
 // set `f`'s spans into the totals, then cleared; threads [0, KC_COUNT) of one workgroup
 __device__ __forceinline__ void kt_fold_set(KStampBlock* blk, int f, uint32_t t) {

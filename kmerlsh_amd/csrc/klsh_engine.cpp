@@ -335,10 +335,17 @@ struct klsh_ctx {
   }
 
   // k_merge_long's bit matrices (runs over 896 rows at d = 16 / 32): one per workgroup, a
-  // workgroup per 897 slots up to 256 (2 MB each)
+  // workgroup per 897 slots up to 256 (2 MB each: up to 512 MB).  None while option long_runs
+  // is 0 (k_merge_huge walks those runs; the matrices are released when it is switched off).
   int ensure_long(uint64_t s, int d_) {
-    const uint32_t want =
-        klsh::long_ok(d_) && s >= 897 ? (uint32_t)std::min<uint64_t>(256, s / 897 + 1) : 0u;
+    const uint32_t want = klsh::long_ok(d_) && s >= 897 && mw.long_off != 1u
+                              ? (uint32_t)std::min<uint64_t>(256, s / 897 + 1)
+                              : 0u;
+    if (want == 0 && mw.long_groups) {
+      dfree(mw.long_P);
+      mw.long_groups = 0;
+      return 0;
+    }
     if (want <= mw.long_groups) return 0;
     dfree(mw.long_P);
     mw.long_groups = 0;
@@ -358,6 +365,8 @@ struct klsh_ctx {
       dp = dp_;
       rows.d = d;
       rows.dp = dp;
+      if (shadow_wanted(d) && !xh_alloc)  // (an earlier load at a width without the image)
+        if (int e = dalloc(&xh_alloc, cap_slots * (uint64_t)cap_dp)) return e;
       rows.xh = shadow_wanted(d) ? xh_alloc : nullptr;
       drop_snapshot();
       return ensure_long(cap_slots, d_);
@@ -1827,7 +1836,8 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   if (n == "long_runs") {
     if (value != 0 && value != 1 && value != 4) return fail(KLSH_E_ARG, "long_runs must be 0, 1 or 4");
     ctx->mw.long_off = value == 1 ? 0u : value == 0 ? 1u : 4u;
-    return 0;
+    KLSH_HIP(hipSetDevice(ctx->device));
+    return ctx->cap_slots ? ctx->ensure_long(ctx->cap_slots, ctx->d) : 0;
   }
   if (n == "wide_image") {
     if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_image must be 0 or 1");

@@ -89,7 +89,9 @@ struct Counters {
 // order) and clears it; the engine folds the last set at the end of a call.
 enum KClass : int {
   KC_PROJECT = 0, KC_SORT, KC_RUNS, KC_SMALL, KC_BIG128, KC_BIG192, KC_BIG384, KC_BIG896, KC_HUGE,
-  KC_TAIL, KC_COMPACT, KC_SCREEN, KC_COUNT
+  KC_TAIL, KC_COMPACT, KC_SCREEN,
+  KC_MERGE,  // (a phase) the merge launches of an iteration at >= 2^20 positions, all classes
+  KC_COUNT
 };
 constexpr int kStampSlots = 16;
 struct alignas(128) StampLine {
@@ -111,8 +113,9 @@ struct KTime {
   KStampBlock* blk;
   int set;
   int fold;
+  int phase = -1;  // >= 0: the launch also stamps this phase class (its first start, last end)
 };
-constexpr KTime kNoTime{nullptr, 0, -1};
+constexpr KTime kNoTime{nullptr, 0, -1, -1};
 // Fold set `t` into the totals and clear it (one workgroup; device code, klsh_device.cuh).
 
 // Merge workspace (device), sized for `cap` positions.

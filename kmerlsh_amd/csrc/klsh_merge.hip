@@ -89,10 +89,14 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
 }
 // v_writelane_b32: lane `l` (a constant after unrolling) of v becomes the wave-uniform value s
 __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t s, int l) {
+#ifdef __OPTIMIZE__
   asm volatile("v_writelane_b32 %0, %1, %2"
                : "=v"(v)
                : "s"(__builtin_amdgcn_readfirstlane(s)), "i"(l), "0"(v));
   return v;
+#else  // (the host-sanitizer build compiles device code at -O0: no constant lane to encode)
+  return (int)__lane_id() == l ? s : v;
+#endif
 }
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
@@ -4077,12 +4081,16 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
   if (n_dev && (lo != 0 || n >= tail_merge_max(w))) return;  // (the caller checks)
   const Decider dc = make_decider(thr);
   if (!runs_ready) launch_runs(key, lo, n, bucket_thr, w, s, n_dev);
+  // the merge phase of a multi-launch iteration is stamped as a whole too (KC_MERGE: the wall of
+  // its concurrent classes, bench.py's roofline phases)
+  MergeWork wm = w;
+  if (w.kt.blk && (n >= tail_merge_max(w) || !project_device_n_ok(r.d))) wm.kt.phase = KC_MERGE;
   switch (r.d) {
-    case 8: launch_groups<8>(r, slots, dc, w, ctr, n, s); break;
-    case 16: launch_groups<16>(r, slots, dc, w, ctr, n, s); break;
-    case 32: launch_groups<32>(r, slots, dc, w, ctr, n, s); break;
-    case 64: launch_groups<64>(r, slots, dc, w, ctr, n, s); break;
-    default: launch_groups_wide(r, slots, dc, w, ctr, n, s);
+    case 8: launch_groups<8>(r, slots, dc, wm, ctr, n, s); break;
+    case 16: launch_groups<16>(r, slots, dc, wm, ctr, n, s); break;
+    case 32: launch_groups<32>(r, slots, dc, wm, ctr, n, s); break;
+    case 64: launch_groups<64>(r, slots, dc, wm, ctr, n, s); break;
+    default: launch_groups_wide(r, slots, dc, wm, ctr, n, s);
   }
 }
 

@@ -5,7 +5,9 @@
 // Reference entry points called (file:line in /root/reference):
 //   Hash::LSH::generateHashTable        hash/lshash.cc:36
 //   Hash::LSH::random_projection        hash/lshash.cc:53
-//   p_cluster                           function/cluster.cc:56
+//   p_lsh / merge_hashtable             function/cluster.cc:4 / :15
+//   p_cluster / nestedCluster           function/cluster.cc:56 / :89
+//   merge_abundance                     function/cluster.cc:39
 //   Cluster                             function/cluster.cc:181
 //   Core::Distance::cosine              function/distance.cc:27
 //   Core::AB::SetConsensus              function/funcAB.cc:49
@@ -28,6 +30,12 @@
 #include "utils/alglib-3.15.0/src/statistics.h"
 
 using namespace std;
+
+// function/cluster.cc:15 defines merge_hashtable with a size_t hash_func_num while cluster.h:31
+// declares it with an int (two different symbols): the definition's signature, to link to it.
+void merge_hashtable(vector<vector<Abundance*>>* final_table, size_t hash_func_num,
+                     const vector<vector<Abundance*>*>& part_hash_values,
+                     const vector<vector<int>*>& part_hash_keys);
 
 static vector<float> read_f32(const char* path, size_t count) {
   vector<float> v(count);
@@ -75,6 +83,8 @@ int main(int argc, char** argv) {
             "  ref_harness cluster ROWS N D MINSIM I BTHR OUTPREFIX\n"
             "  ref_harness cluster_from BINPREFIX D MINSIM I BTHR OUTPREFIX   (input via ReadClusterAll)\n"
             "  ref_harness cluster_w ROWS OFF IDS N D MINSIM I BTHR OUTPREFIX (binary member lists)\n"
+            "  ref_harness iter_w ROWS OFF IDS N D THR BTHR  (ONE iteration of Cluster's body at\n"
+            "                                               threshold THR, timed; no output files)\n"
             "  ref_harness convert COUNTS N D VKMERS OUTPREFIX  (uint16 sample-major counts -> convertHTMat)\n"
             "  ref_harness ttest VALUES N M COUNT OUT       (f32 cases of N+M values -> studentttest2,\n"
             "                                               f64 bothtails/lefttail/righttail per case)\n");
@@ -144,11 +154,11 @@ int main(int argc, char** argv) {
     write_bytes(argv[6], c._values.data(), (size_t)d * 4);
     return 0;
   }
-  if (cmd == "cluster" || cmd == "cluster_from" || cmd == "cluster_w") {
+  if (cmd == "cluster" || cmd == "cluster_from" || cmd == "cluster_w" || cmd == "iter_w") {
     vector<Abundance*> v;
     int argi;
     int d;
-    if (cmd == "cluster_w") {  // ROWS.f32 OFF.u64 IDS.u64 N D ...: rows with member-id lists
+    if (cmd == "cluster_w" || cmd == "iter_w") {  // ROWS.f32 OFF.u64 IDS.u64 N D ...: rows with member-id lists
       const size_t n = strtoull(argv[5], nullptr, 10);
       d = atoi(argv[6]);
       vector<float> x = read_f32(argv[2], n * d);
@@ -179,13 +189,64 @@ int main(int argc, char** argv) {
       IOMat::ReadClusterAll(&v, d, argv[2], false);
       argi = 4;
     }
-    const float min_sim = (float)atof(argv[argi]);
-    const int iters = atoi(argv[argi + 1]);
-    const int bthr = atoi(argv[argi + 2]);
     // threads_to_use: 1 (T=1 semantics, deterministic) unless KLSH_REF_THREADS asks for more
     // (timing only: at T>1 the reference's bucket order depends on scheduling, cluster.cc:281)
     const char* te = getenv("KLSH_REF_THREADS");
-    const unsigned threads = te ? (unsigned)atoi(te) : 1u;
+    const unsigned threads = te ? std::max(1, atoi(te)) : 1u;
+    if (cmd == "iter_w") {
+      // One pass of Cluster()'s loop body (function/cluster.cc:199-331) at the caller's threshold
+      // — Cluster() itself always starts its schedule at 0.95 (:190) — through the reference's
+      // own p_lsh, merge_hashtable, p_cluster / nestedCluster and merge_abundance, with the same
+      // OpenMP structure, so bench.py can time an iteration of the loop at its scheduled value.
+      const float thr = (float)atof(argv[argi]);
+      const int bthr = atoi(argv[argi + 1]);
+      const size_t n0 = v.size();
+      const auto t0 = chrono::high_resolution_clock::now();
+      const size_t h = floor(log2(v.size()));
+      const size_t buckets = size_t(pow(2, h));
+      vector<vector<Abundance*>> table(buckets, vector<Abundance*>());
+      hashTable ht = LSH::generateHashTable(h, d);
+      vector<vector<Abundance*>*> pv;
+      vector<vector<int>*> pk;
+      for (unsigned i = 0; i < threads; ++i) {
+        pv.push_back(new vector<Abundance*>());
+        pk.push_back(new vector<int>());
+      }
+      const int na = (int)v.size();
+#pragma omp parallel for num_threads(threads)
+      for (int i = 0; i < na; ++i) p_lsh(pv[omp_get_thread_num()], pk[omp_get_thread_num()], ht, v[i]);
+      merge_hashtable(&table, h, pv, pk);
+      for (unsigned i = 0; i < threads; ++i) {
+        delete pv[i];
+        delete pk[i];
+      }
+      vector<vector<Abundance*>*> part;
+      for (unsigned i = 0; i < threads; ++i) part.push_back(new vector<Abundance*>());
+      omp_set_nested(1);
+      omp_set_max_active_levels(2);
+#pragma omp parallel for num_threads(threads) schedule(dynamic)
+      for (size_t s = 0; s < buckets; ++s) {
+        auto& cand = table[s];
+        const int tid = omp_get_thread_num();
+        if (cand.size() > (size_t)bthr) {
+          nestedCluster(&cand, thr, d, 3, false);
+          part[tid]->insert(part[tid]->end(), cand.begin(), cand.end());
+        } else {
+          p_cluster(part[tid], &cand, thr);
+        }
+      }
+      omp_set_nested(0);
+      merge_abundance(&v, part);
+      for (unsigned i = 0; i < threads; ++i) delete part[i];
+      const double secs =
+          chrono::duration<double>(chrono::high_resolution_clock::now() - t0).count();
+      printf("iteration: %zu -> %zu rows at threshold %.9g, %u threads\n", n0, v.size(), thr, threads);
+      printf("one iteration takes (secs): %.6f\n", secs);
+      return 0;
+    }
+    const float min_sim = (float)atof(argv[argi]);
+    const int iters = atoi(argv[argi + 1]);
+    const int bthr = atoi(argv[argi + 2]);
     Cluster(&v, min_sim, iters, threads ? threads : 1u, d, bthr, true);
     save(&v, argv[argi + 3]);
     return 0;

@@ -338,21 +338,22 @@ def test_pcluster_run_lengths_vs_oracle(engine, oracle, b, d, groups, noise, thr
     assert_same_result(engine.result(), *oracle.pcluster(rows, thr))
 
 
-@pytest.mark.parametrize("b,d,groups,noise,thr", [
-    (3000, 32, 100, 0.05, 0.9), (2500, 64, 300, 0.08, 0.85), (1500, 16, 20, 0.03, 0.95),
-    (1200, 512, 40, 0.05, 0.9), (9000, 8, 900, 0.1, 0.8), (2000, 100, 2, 0.01, 0.9)])
-def test_pcluster_huge_runs_folded_vs_oracle(engine, oracle, b, d, groups, noise, thr):
+@pytest.mark.parametrize("b,d,groups,noise,thr,long_runs", [
+    (3000, 32, 100, 0.05, 0.9, 1), (3000, 32, 100, 0.05, 0.9, 0), (2500, 64, 300, 0.08, 0.85, 4),
+    (1500, 16, 20, 0.03, 0.95, 1), (1500, 16, 20, 0.03, 0.95, 0), (1200, 512, 40, 0.05, 0.9, 4),
+    (9000, 8, 900, 0.1, 0.8, 4), (2000, 100, 2, 0.01, 0.9, 4)])
+def test_pcluster_huge_runs_folded_vs_oracle(engine, oracle, b, d, groups, noise, thr, long_runs):
     """Runs over 896 rows walked by the 385..896-row kernel's 256-lane workgroups (option
-    "huge_fold", what the loop does after iterations without such runs) instead of k_merge_huge."""
+    "huge_fold", what the loop does after iterations without such runs) instead of k_merge_huge
+    — through the per-class launches (tail_merge_rows = 1: k_merge_tail has no fold), and at
+    d = 16 / 32 with k_merge_long off for them (long_runs 1: only >896-row runs would be its;
+    0: none), which is where the fold takes over there."""
     rng = np.random.default_rng(b * 3 + d)
     rows = clustered(rng, b, d, groups, noise)
-    engine.set_option("huge_fold", 1)
-    try:
+    with options(engine, huge_fold=1, tail_merge_rows=1, long_runs=long_runs):
         engine.load_rows(rows)
         engine.pcluster(thr)
         got = engine.result()
-    finally:
-        engine.set_option("huge_fold", 0)
     assert_same_result(got, *oracle.pcluster(rows, thr))
 
 
@@ -646,22 +647,31 @@ def test_cluster_random_vs_oracle(engine, oracle, n, d, groups, iters, bthr):
     assert_same_result(engine.result(), o_rows, o_off, o_ids)
 
 
-@pytest.mark.parametrize("n,d,groups,iters,bthr", [(50000, 16, 3, 3, 5000), (60000, 32, 20, 4, 1000000)])
-def test_cluster_huge_fold_vs_oracle(engine, oracle, n, d, groups, iters, bthr):
+@pytest.mark.parametrize("n,d,groups,iters,bthr,long_runs", [
+    (50000, 16, 3, 3, 5000, 4), (60000, 32, 20, 4, 1000000, 4), (60000, 32, 20, 4, 1000000, 1),
+    (60000, 32, 20, 4, 1000000, 0), (50000, 16, 10, 3, 1000000, 0), (60000, 8, 20, 4, 1000000, 4),
+    (60000, 64, 20, 4, 1000000, 4)])
+def test_cluster_huge_fold_vs_oracle(engine, oracle, n, d, groups, iters, bthr, long_runs):
     """The loop with every >896-row run walked inside the 385..896-row kernel (option huge_fold),
-    nested buckets included."""
+    nested buckets included, through the per-class launches (tail_merge_rows = 1).  Where the fold
+    is the path (every width but d = 16 / 32 with long_runs = 4, whose >384-row runs are
+    k_merge_long's) no launch of the >896-row class is made although such runs exist: the fold
+    walked them."""
     rng = np.random.default_rng(n + d + 1)
     rows = clustered(rng, n, d, groups, 0.05)
-    engine.set_option("huge_fold", 1)
-    try:
+    with options(engine, huge_fold=1, tail_merge_rows=1, long_runs=long_runs):
         engine.load_rows(rows)
-        trace, counter, _ = engine.cluster(0.8, iters, bthr, 777, 3)
+        trace, counter, st = engine.cluster(0.8, iters, bthr, 777, 3)
         got = engine.result()
-    finally:
-        engine.set_option("huge_fold", 0)
     o_rows, o_off, o_ids, o_trace, o_counter = oracle.cluster(rows, 0.8, iters, bthr, 777, 3)
     assert np.array_equal(trace, o_trace) and counter == o_counter
     assert_same_result(got, o_rows, o_off, o_ids)
+    huge = st["kern"]["huge"]
+    assert huge["runs"] > 0  # runs over 896 rows were listed
+    if d in (16, 32) and long_runs == 4:
+        assert huge["launches"] > 0  # k_merge_long
+    else:
+        assert huge["launches"] == 0  # folded into the 385..896-row kernel
 
 
 @pytest.mark.parametrize("window", [7, 40, 100])

@@ -104,3 +104,42 @@ def test_io_roundtrip(tmp_path):
     r2, o2, i2 = kio.read_cluster_all(str(tmp_path / "r.txt"), 6)
     assert np.array_equal(r2, rows[[0, 1, 3]])
     assert list(np.diff(o2)) == [6, 7, 6]
+
+
+@pytest.mark.gpu
+def test_stats_struct_size_is_checked(tmp_path):
+    """A caller built against another klsh.h (a statistics struct of another size) is refused with
+    KLSH_E_ARG before anything is written into its struct: klsh_cluster, klsh_extract_fastq and
+    klsh_build_khtable (include/klsh.h, ABI v2+ struct_size)."""
+    import ctypes
+
+    from kmerlsh_amd import _native
+
+    lib = _native.load_library()
+    with _native.Engine(0) as eng:
+        rows = np.random.default_rng(3).random((256, 16), dtype=np.float32)
+        eng.load_rows(rows)
+        for cls, call in [
+            (_native.KlshStats,
+             lambda st: lib.klsh_cluster(eng._ctx, ctypes.c_float(0.9), 2, 1000, 12345,
+                                         ctypes.byref(ctypes.c_uint64(0)), None, ctypes.byref(st))),
+            (_native.KlshKhtableStats,
+             lambda st: lib.klsh_build_khtable(eng._ctx, (ctypes.c_char_p * 1)(b"missing"), 1, 31,
+                                               str(tmp_path).encode(), ctypes.byref(st))),
+        ]:
+            st = cls()
+            st.struct_size = ctypes.sizeof(st) - 8
+            assert call(st) == -1, cls.__name__  # KLSH_E_ARG
+            assert st.struct_size == ctypes.sizeof(st) - 8  # untouched
+        ks = _native.KmerSet(eng, np.arange(1, 9, dtype=np.uint64))
+        try:
+            st = _native.KlshExtractStats()
+            st.struct_size = ctypes.sizeof(st) - 8
+            fq = tmp_path / "r.fq"
+            fq.write_bytes(b"@r\nACGT\n+\nIIII\n")
+            rc = lib.klsh_extract_fastq(eng._ctx, ks._set, str(fq).encode(),
+                                        str(tmp_path / "o.fq").encode(), 3, ctypes.c_float(0.5),
+                                        ctypes.byref(st))
+            assert rc == -1
+        finally:
+            ks.close()
