@@ -162,8 +162,8 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
     """The reference (oracle/_ref/ref_harness: the reference's own functions, compiled from its
     sources) or the oracle port, timed on this host's cores.
 
-    Default (a bounded sample): one iteration of the loop from its own state at t = 0, .1 I, .2 I,
-    .4 I, .6 I, .9 I (the engine provides the state) at the schedule's threshold for t — the
+    Default (a bounded sample): one iteration of the loop from its own state at 14 points t in
+    [0, .9 I] (the engine provides the state) at the schedule's threshold for t — the
     harness's iter_w, Cluster()'s loop body through the reference's p_lsh, merge_hashtable,
     p_cluster / nestedCluster and merge_abundance (Cluster() itself would start at 0.95).  Its
     per-row cost, interpolated in t and weighted by the loop's N_t trace, estimates T_loop; value
@@ -192,10 +192,22 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
             del rows, off, ids
             log(f"cpu baseline: the reference's whole loop, {iters} iterations from {n_t} rows, "
                 f"{threads} threads")
-            out = subprocess.run([harness, "cluster_w", src, src + ".off", src + ".ids", str(n_t),
-                                  str(d), repr(float(min_sim)), str(iters), "1000000",
-                                  os.path.join(tmp, "out")], env=env, check=True,
-                                 capture_output=True, text=True, timeout=3000).stdout
+            # (its verbose output streamed: a progress line every 25 iterations keeps a long run
+            # visibly alive)
+            proc = subprocess.Popen([harness, "cluster_w", src, src + ".off", src + ".ids",
+                                     str(n_t), str(d), repr(float(min_sim)), str(iters), "1000000",
+                                     os.path.join(tmp, "out")], env=env, stdout=subprocess.PIPE,
+                                    text=True)
+            lines = []
+            for ln in proc.stdout:
+                lines.append(ln)
+                if ln.startswith("Iteration:"):
+                    it = int(ln.split()[1].rstrip(","))
+                    if it % 25 == 0:
+                        log(f"cpu baseline: reference iteration {it}/{iters}")
+            if proc.wait(timeout=3000) != 0:
+                raise RuntimeError(f"ref_harness cluster_w exited with {proc.returncode}")
+            out = "".join(lines)
         secs = float(re.findall(r"hash\+cluster takes \(secs\): ([0-9.eE+-]+)", out)[-1])
         sizes = [int(v) for v in re.findall(r"Size of profilings\D*(\d+)", out)]
         log(f"cpu baseline: reference loop {secs:.1f} s")
@@ -204,7 +216,9 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
         full = {"value": n0 * iters / secs, "loop_s": secs, "sum_trace": int(sum(sizes[-iters:])),
                 "final_rows": int(re.findall(r"after clustering:\s*(\d+)", out)[-1])}
     trace = np.asarray(trace, dtype=np.float64)
-    ts = sorted({min(iters - 1, int(f * iters)) for f in (0.0, 0.1, 0.2, 0.4, 0.6, 0.9)})
+    # 14 points, densest where N_t and the per-row cost change fastest (the head)
+    ts = sorted({min(iters - 1, int(f * iters))
+                 for f in (0.0, 0.05, 0.1, 0.15, 0.2, 0.25, 0.3, 0.35, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9)})
     cost, secs_all = [], 0.0
     for t in ts:
         rows, off, ids = state_at(eng, t, min_sim, iters, counter0)
