@@ -1871,6 +1871,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     return 0;
   }
   if (n == "tail_screen_grid") return grid(&ctx->mw.tail_screen_grid);
+  if (n == "tail_big_screen") {
+    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "tail_big_screen must be 0 or 1");
+    ctx->mw.tail_big_screen = (uint32_t)value;
+    return 0;
+  }
   if (n == "small_screen") {
     if (value != 0 && value != 1) return fail(KLSH_E_ARG, "small_screen must be 0 or 1");
     ctx->mw.small_screen = (uint32_t)value;
@@ -1906,6 +1911,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "small_screen") *value = ctx->mw.small_screen;
   else if (n == "tail_screen") *value = ctx->mw.tail_screen;
   else if (n == "tail_screen_grid") *value = ctx->mw.tail_screen_grid;
+  else if (n == "tail_big_screen") *value = ctx->mw.tail_big_screen;
   else if (n == "wide_image") *value = ctx->wide_image;
   else if (n == "long_runs") *value = ctx->mw.long_off == 1u ? 0 : ctx->mw.long_off == 0u ? 1 : ctx->mw.long_off;
   else if (n == "wide_projection") *value = ctx->pw.wide_h16;

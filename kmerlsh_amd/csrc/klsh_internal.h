@@ -171,6 +171,12 @@ struct MergeWork {
   // "tail_screen": 1 = the small-run screen also runs in front of k_merge_tail (iterations below
   // tail_merge_rows), whose small-run waves then walk only the runs it passed
   uint32_t tail_screen = 1;
+  // "tail_big_screen": 1 = there, k_merge_tail's 65..384-row runs are first screened on the fp16
+  // image in their workgroup (the small-run screen's certified test); a run with no pair left
+  // reads no f32 row.  big_screen / bs_*: set per launch (the test's threshold and margins).
+  uint32_t tail_big_screen = 1;
+  uint32_t big_screen = 0;
+  float bs_s_star = 0.0f, bs_m0 = 0.0f, bs_a2 = 0.0f;
   uint32_t tail_screen_grid;  // "tail_screen_grid": its persistent launch there (0: 2048)
   // "tail_merge_rows": below this many positions every merge class runs in ONE launch
   // (k_merge_tail); 0 = the default 2^20 (tests lower it to reach the per-class launches)

@@ -62,7 +62,12 @@ __device__ unsigned long long g_wprof[8][8];  // walk phases in shader clocks: f
 __device__ unsigned long long g_gprof[8];  // Gram tiles: tiles, ambiguous pairs, sum of the wave's
                                            // longest lane list, clocks: acc, screen, exact, bits
 #define GPROF_ADD(k, v) atomicAdd(&g_gprof[k], (unsigned long long)(v))
+__device__ unsigned long long g_tprof[8];  // k_tail_local phases (10-ns ticks summed over
+                                           // workgroups): base, counts, lists, scatter; workgroups;
+                                           // max total
+#define TPROF_ADD(k, v) atomicAdd(&g_tprof[k], (unsigned long long)(v))
 #else
+#define TPROF_ADD(k, v) (void)0
 #define GPROF_ADD(k, v) (void)0
 #define MPROF_T() 0ull
 #define MPROF_ADD(c, k, v) (void)0
@@ -1231,6 +1236,7 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t d = blockIdx.x;
   const uint32_t RAD = 1u << lb, MASK = RAD - 1u;
+  [[maybe_unused]] uint64_t tp0 = MPROF_T(), tp1 = 0;
   // the bucket: [base, base + m) of the partition
   // (every global load of this kernel is unconditional, index clamped into range: a load under a
   // branch is waited for at once, and these few-hundred-key buckets are a chain of round trips)
@@ -1257,6 +1263,9 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     kt_end(w.kt, KC_RUNS);
     return;
   }
+#ifdef KLSH_MERGE_PROF
+  if (t == 0) { tp1 = MPROF_T(); TPROF_ADD(0, tp1 - tp0); TPROF_ADD(4, 1); }
+#endif
   // 1. low-digit counts (4 keys a thread per round, loads first)
   for (uint32_t i0 = 0; i0 < m; i0 += 1024u) {
     uint32_t kk[4];
@@ -1270,6 +1279,9 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
       if (i0 + (uint32_t)q * 256u + t < m) atomicAdd(&cnt[kk[q] & MASK], 1u);
   }
   __syncthreads();
+#ifdef KLSH_MERGE_PROF
+  if (t == 0) { const uint64_t x = MPROF_T(); TPROF_ADD(1, x - tp1); tp1 = x; }
+#endif
   // 2. the runs (digits with a count >= 2) per list, and the digit starts
   uint32_t c4[4], acc = 0, heads = 0, small_rows = 0;
   uint32_t lrows[kBigClasses + 1] = {};
@@ -1332,6 +1344,10 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     }
   }
   // 3. the stable scatter, 4096 keys per round (wave wv: positions wv*1024 + j*64 + lane)
+#ifdef KLSH_MERGE_PROF
+  __syncthreads();
+  if (t == 0) { const uint64_t x = MPROF_T(); TPROF_ADD(2, x - tp1); tp1 = x; }
+#endif
   const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   for (uint32_t r0 = 0; r0 < m; r0 += kChunk) {
     uint32_t k[kItems], v[kItems], lr[kItems];
@@ -1380,6 +1396,13 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     for (uint32_t dg = t; dg < RAD; dg += 256) wc[0][dg] = wc[1][dg] = wc[2][dg] = wc[3][dg] = 0u;
     __syncthreads();
   }
+#ifdef KLSH_MERGE_PROF
+  if (t == 0) {
+    const uint64_t x = MPROF_T();
+    TPROF_ADD(3, x - tp1);
+    atomicMax(&g_tprof[5], (unsigned long long)(x - tp0));
+  }
+#endif
   kt_end(w.kt, KC_RUNS);
 }
 
@@ -2186,14 +2209,111 @@ struct BigLayout {
   static constexpr size_t bytes = meta + sizeof(uint32_t) * RB * 8;
 };
 
+// The fp16 screen of one big run (k_merge_tail, option tail_big_screen): k_small_screen's certified
+// test (screen_margins) over every pair of the run's image rows, 32 x 32 blocks on
+// v_mfma_f32_32x32x16_f16.  Returns whether the run can merge at all (some pair not ruled out, or a
+// row whose image has no usable norm); false: the walk would change nothing — no f32 row is read.
+// slot[0, b): the run's slots (LDS); hrows: room for b x (D + 8) halves; linv: b floats.
+template <int D, int NT>
+__device__ __forceinline__ bool big_screen_pass(uint32_t b, const uint32_t* slot, const Rows& r,
+                                                float s_star, float m0, float a2,
+                                                _Float16* hrows, float* linv, uint32_t* flag) {
+  constexpr int STH = D + 8, LPR = D / 8, NW = NT / 64;  // a lane loads 16 B = 8 halves
+  constexpr uint32_t RPR = NT / LPR;                      // rows per round
+  constexpr int KB = 4;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  if (t == 0) *flag = 0u;
+  {
+    const uint32_t sub = (t % LPR) * 8u, rr = t / LPR;
+    const uint32_t rounds = (b + RPR - 1u) / RPR;
+    for (uint32_t g0 = 0; g0 < rounds; g0 += KB) {  // block-uniform
+      sh16x8 v[KB];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const uint32_t a = min((g0 + (uint32_t)k) * RPR + rr, b - 1u);
+        v[k] = *reinterpret_cast<const sh16x8*>(r.xh + (size_t)slot[a] * r.dp + sub);
+      }
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const uint32_t a = (g0 + (uint32_t)k) * RPR + rr;
+        if (a < b) *reinterpret_cast<sh16x8*>(hrows + a * STH + sub) = v[k];
+      }
+    }
+  }
+  lds_barrier();
+  bool bad = false;
+  for (uint32_t a = t; a < b; a += NT) {  // |x~|, as k_small_screen computes it
+    float ss = 0.0f;
+#pragma unroll
+    for (int q = 0; q < D / 8; ++q) {
+      const sh16x8 x = *reinterpret_cast<const sh16x8*>(hrows + a * STH + 8 * q);
+#pragma unroll
+      for (int h2 = 0; h2 < 8; h2 += 2) {
+        const sh16x2 v = {x[h2], x[h2 + 1]};
+        ss = __builtin_amdgcn_fdot2(v, v, ss, false);
+      }
+    }
+    const bool bd = !(ss >= 0x1p-100f && ss <= 0x1p100f);
+    bad = bad || bd;
+    linv[a] = bd ? 0.0f : 1.0f / __builtin_sqrtf(ss);
+  }
+  if (bad) *flag = 1u;
+  lds_barrier();
+  if (*flag) return true;  // (block-uniform) a row the image cannot carry: the exact merge
+  const uint32_t nb = (b + 31u) / 32u, r32 = lane & 31u, k8 = 8u * (lane >> 5);
+  const uint32_t ntiles = nb * (nb + 1u) / 2u;
+  bool fail = false;
+  for (uint32_t ti = wv; ti < ntiles; ti += NW) {  // wave-uniform: blocks tr <= tc
+    uint32_t tc = (uint32_t)((__builtin_sqrtf(8.0f * (float)ti + 1.0f) - 1.0f) * 0.5f);
+    while (tc * (tc + 1u) / 2u > ti) --tc;
+    while ((tc + 1u) * (tc + 2u) / 2u <= ti) ++tc;
+    const uint32_t tr = ti - tc * (tc + 1u) / 2u;
+    pf16acc acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+    const uint32_t ra = min(tr * 32u + r32, b - 1u), ca = min(tc * 32u + r32, b - 1u);
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      const sh16x8 fa = *reinterpret_cast<const sh16x8*>(hrows + ra * STH + 16 * ks + k8);
+      const sh16x8 fb = *reinterpret_cast<const sh16x8*>(hrows + ca * STH + 16 * ks + k8);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
+    }
+    const uint32_t C = tc * 32u + r32;
+    const float ic = linv[ca];
+    float4 irv[4];  // rows tr*32 + 8j + 4h + (0..3)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      irv[j] = *reinterpret_cast<const float4*>(linv + min(tr * 32u + 8u * (uint32_t)j + 4u * (lane >> 5), (b - 1u) & ~3u));
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t R = tr * 32u + (uint32_t)(q & 3) + 8u * (uint32_t)(q >> 2) + 4u * (lane >> 5);
+      const float4 v = irv[q >> 2];
+      const float ir = (q & 3) == 0 ? v.x : (q & 3) == 1 ? v.y : (q & 3) == 2 ? v.z : v.w;
+      const float qv = acc[q] * ir * ic;
+      const float m = m0 + a2 * (ir + ic);
+      fail = fail | ((R < C) & (C < b) & !(qv < s_star - m));  // NaN / inf: not ruled out
+    }
+  }
+  if (fail) *flag = 1u;
+  lds_barrier();
+  return *flag != 0u;
+}
+
+struct BigScreen {
+  uint32_t on;
+  float s_star, m0, a2;
+};
+
 // The runs li = first, first + stride, ... (< count) of list `list` (size class cls), one
 // workgroup of NT lanes per run, with smem = BigLayout<D, RB, ROWS_LDS>::bytes of LDS.
+// bs.on (k_merge_tail, d = 32 / 64 with the fp16 image): each run is screened first
+// (big_screen_pass) and left alone when no pair of it can merge.
 template <int D, int RB, int NT, bool ROWS_LDS>
 __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls, uint32_t count,
                                          uint32_t first, uint32_t stride,
                                          uint32_t* __restrict__ slots, const Decider& dc,
                                          const Rows& r, Counters* ctr, uint32_t* dlist,
-                                         unsigned char* smem) {
+                                         unsigned char* smem, BigScreen bs = BigScreen{0u, 0.0f, 0.0f, 0.0f}) {
   using L = BigLayout<D, RB, ROWS_LDS>;
   constexpr int ST = L::ST, W = L::W, NW = NT / 64;
   float* rows = reinterpret_cast<float*>(smem + L::rows);  // rows, or one staged column block
@@ -2240,6 +2360,22 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
       uint32_t sl[KA], mc[KA], mh[KA], mt[KA];
 #pragma unroll
       for (int ka = 0; ka < KA; ++ka) sl[ka] = slots[p + min(t + (uint32_t)ka * NT, b - 1u)];
+      if constexpr (D == 32 || D == 64) {
+        if (bs.on) {  // (uniform) the fp16 screen first: a run that cannot merge is left as it is
+          __shared__ uint32_t sflag;
+#pragma unroll
+          for (int ka = 0; ka < KA; ++ka) {
+            const uint32_t a = t + (uint32_t)ka * NT;
+            if (a < b) slot[a] = sl[ka];
+          }
+          lds_barrier();
+          if (!big_screen_pass<D, NT>(b, slot, r, bs.s_star, bs.m0, bs.a2,
+                                      reinterpret_cast<_Float16*>(rows), sq, &sflag)) {
+            __syncthreads();
+            continue;
+          }
+        }
+      }
 #pragma unroll
       for (int ka = 0; ka < KA; ++ka) {
         mc[ka] = r.cnt[sl[ka]];
@@ -2458,6 +2594,7 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
     // 385..896, 193..384, 129..192, 65..128
     const uint32_t a4 = nh, a3 = a4 + cnt[3], a2 = a3 + cnt[2], a1 = a2 + cnt[1],
                    total = a1 + cnt[0];
+    const BigScreen bs{w.big_screen, w.bs_s_star, w.bs_m0, w.bs_a2};
     for (uint32_t li = blockIdx.x; li < total; li += nbig) {  // block-uniform
       if (li < a4)
         huge_runs<D, 256>(w.huge, li + 1, li, 1u << 30, slots, dc, r, w, ctr, smem);
@@ -2466,13 +2603,13 @@ __global__ __launch_bounds__(256) void k_merge_tail(MergeWork w, uint32_t* __res
                                      ctr, w.dlist, smem);
       else if (li < a2)
         big_runs<D, 384, 256, true>(w.big[2], 2, li - a3 + 1, li - a3, 1u << 30, slots, dc, r, ctr,
-                                    w.dlist, smem);
+                                    w.dlist, smem, bs);
       else if (li < a1)
         big_runs<D, 192, 256, true>(w.big[1], 1, li - a2 + 1, li - a2, 1u << 30, slots, dc, r, ctr,
-                                    w.dlist, smem);
+                                    w.dlist, smem, bs);
       else
         big_runs<D, 128, 256, true>(w.big[0], 0, li - a1 + 1, li - a1, 1u << 30, slots, dc, r, ctr,
-                                    w.dlist, smem);
+                                    w.dlist, smem, bs);
       __syncthreads();
     }
   } else {
@@ -3889,6 +4026,12 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
     const uint32_t nbig = w.tail_nbig ? w.tail_nbig : 128u;
     const uint32_t nsmall = w.tail_nsmall ? w.tail_nsmall : 512u;
     MergeWork wt = w;
+    wt.big_screen = 0u;
+    if (w.tail_big_screen && screen_ok(r, dc, w)) {
+      screen_margins(r.d, &wt.bs_m0, &wt.bs_a2);
+      wt.bs_s_star = dc.s_star;
+      wt.big_screen = 1u;
+    }
     if (w.tail_screen && screen_ok(r, dc, w)) {
       // the fp16 screen of the small runs first (few of them merge this late in the loop), on
       // the same stream: k_merge_tail's small-run waves then take only the runs it passed
@@ -4133,7 +4276,13 @@ void merge_prof_dump(FILE* f) {
                " close pairs %llu (longest lane %.2f per slow tile), exact loop clocks/slow tile %.0f\n",
             g[7], (double)g[3] / g[7], (double)g[4] / g[7], g[0], g[1], (double)g[2] / g[0],
             (double)g[5] / g[0]);
+  unsigned long long tq[8];
+  if (hipMemcpyFromSymbol(tq, HIP_SYMBOL(g_tprof), sizeof(tq)) == hipSuccess && tq[4])
+    fprintf(f, "[tprof] k_tail_local workgroups %llu  per workgroup us: base %.2f  counts %.2f  lists %.2f"
+               "  scatter %.2f  (max total %.2f)\n", tq[4], tq[0] * 1e-2 / tq[4], tq[1] * 1e-2 / tq[4],
+            tq[2] * 1e-2 / tq[4], tq[3] * 1e-2 / tq[4], tq[5] * 1e-2);
   unsigned long long z[8][12] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tprof), z, sizeof(tq));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gprof), z, sizeof(g));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_mprof), z, sizeof(z));
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), z, sizeof(unsigned long long) * 64);

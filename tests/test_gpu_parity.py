@@ -802,3 +802,42 @@ def test_full_size_c2_properties(engine):
     rows2, off2, ids2 = engine.result()
     assert np.array_equal(trace, trace2) and c1 == c2
     assert np.array_equal(off, off2) and np.array_equal(ids, ids2) and same_bits(rows, rows2)
+
+
+@pytest.mark.parametrize("b,d,groups,noise,thr,special", [
+    (70, 64, 4, 0.05, 0.999, False), (70, 64, 4, 0.05, 0.9, False), (200, 64, 6, 0.08, 0.99, True),
+    (384, 64, 3, 0.05, 0.995, True), (384, 64, 3, 0.05, 0.8, False), (130, 32, 5, 0.05, 0.995, True),
+    (300, 32, 200, 0.3, 0.9, False), (128, 32, 2, 0.01, 0.9, True)])
+@pytest.mark.parametrize("screen", [1, 0])
+def test_tail_big_screen_vs_oracle(engine, oracle, b, d, groups, noise, thr, special, screen):
+    """Option tail_big_screen (default 1): a 65..384-row run in k_merge_tail is screened on the fp16
+    image first and left alone when no pair can pass — merge-free runs (thresholds close to 1),
+    merge-dense runs, and rows the image cannot carry (fp16 overflow, all-zero image of a nonzero
+    row, zero, NaN), with the screen on and off: the oracle's result bit for bit."""
+    rng = np.random.default_rng(b * 13 + d + int(thr * 1000))
+    rows = clustered(rng, b, d, groups, noise)
+    if special:
+        rows[5] *= np.float32(1e5)      # fp16 overflow in the image
+        rows[9] *= np.float32(1e-9)     # image all zero
+        rows[11] = 0.0
+        rows[17, 3] = np.nan
+    with options(engine, tail_big_screen=screen):
+        engine.load_rows(rows)
+        engine.pcluster(thr)
+        got = engine.result()
+    assert_same_result(got, *oracle.pcluster(rows, thr))
+
+
+@pytest.mark.parametrize("d", [32, 64])
+def test_cluster_tail_big_screen_vs_oracle(engine, oracle, d):
+    """The loop through k_merge_tail with big runs (tight groups, thresholds stepping down from
+    0.95): every iteration's 65..384-row runs screened on the fp16 image first."""
+    rng = np.random.default_rng(d + 99)
+    rows = clustered(rng, 120000, d, 600, 0.03)
+    want = oracle.cluster(rows, 0.8, 10, 1000000, 17, 2)
+    engine.load_rows(rows)
+    trace, counter, st = engine.cluster(0.8, 10, 1000000, 17, 2)
+    assert st["kern"]["tail"]["launches"] == 10
+    assert sum(st["kern"][c]["runs"] for c in ("big128", "big192", "big384")) == 0  # all in the tail
+    assert np.array_equal(trace, want[3]) and counter == want[4]
+    assert_same_result(engine.result(), *want[:3])
