@@ -634,6 +634,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
   constexpr uint32_t kBuf = 256;                  // passed runs kept in LDS before a flush
   __shared__ __attribute__((aligned(16))) _Float16 lrow[64 * STH];
   __shared__ __attribute__((aligned(16))) float linv[64];
+  __shared__ __attribute__((aligned(16))) float lsrow[64];  // s* - (m0 + a2 / |x~|): the row's part
   __shared__ uint32_t lflag[64];  // per run of the batch: some pair not ruled out
   __shared__ uint2 buf[kBuf];     // passed runs (start, length | class << 16)
   __shared__ uint32_t fcnt[NC], fbase[NC];
@@ -736,7 +737,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
     // goes to the exact merge
     const bool bad = valid && !(ss >= 0x1p-100f && ss <= 0x1p100f);
     const uint32_t lg = (uint32_t)__builtin_ctz(G);  // log2 G
-    linv[lane] = valid && !bad ? 1.0f / __builtin_sqrtf(ss) : 0.0f;
+    const float il = valid && !bad ? 1.0f / __builtin_sqrtf(ss) : 0.0f;
+    linv[lane] = il;
+    lsrow[lane] = s_star - (m0 + a2 * il);
     lflag[lane] = 0u;
     wave_lds_fence();
     if (bad) lflag[lane >> lg] = 1u;
@@ -744,14 +747,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
     // The Gram blocks of the batch's runs on the matrix cores (x~ . x~ exact products, f32 sums):
     // 32 x 32 tiles for runs of 17..64 rows (the upper-triangular tiles of each run), 16 x 16
     // diagonal tiles for shorter runs (4 per batch, runs never cross a 16-row block).  A pair
-    // (R < C) of one run that the screen cannot rule out flags the run in LDS.  The tests of a
-    // lane's tile entries are branch-free over inverse norms loaded up front (a load inside each
-    // test's branch was a wait on LDS per entry); the flag store is the only predicated step.
-    auto test = [&](uint32_t R, uint32_t C, float sv, float ir, float ic) -> bool {
-      const bool pair = (R < C) & ((R >> lg) == (C >> lg)) & (((vmask >> R) & (vmask >> C) & 1ull) != 0ull);
-      const float qv = sv * ir * ic;
-      const float m = m0 + a2 * (ir + ic);
-      return pair & !(qv < s_star - m);  // NaN / inf: not ruled out
+    // (R < C) of one run that the screen cannot rule out flags the run in LDS.  The tests are
+    // branch-free over per-row terms loaded up front (a load inside each test's branch was a wait
+    // on LDS per entry): a pair is ruled out when G/(|x~a||x~b|) < s* - (m0 + a2 (1/|x~a| +
+    // 1/|x~b|)), evaluated as (G ir) ic < lsrow[R] - a2 ic — the margin's terms summed in another
+    // order, a few ulps of s* against the margin's 1.5x headroom; pair validity is one per-lane
+    // mask per tile, applied once to the tile's failures.
+    auto test = [&](float sv, float ir, float sr, float ic, float kc) -> bool {
+      return !(sv * ir * ic < sr - kc);  // NaN / inf: not ruled out
+    };
+    // bits (q & 3) + 8 (q >> 2) of w -> bit q (the tile rows of a lane, 32 x 32 layout)
+    auto rows16 = [](uint32_t w) -> uint32_t {
+      return (w & 0xFu) | ((w >> 4) & 0xF0u) | ((w >> 8) & 0xF00u) | ((w >> 12) & 0xF000u);
     };
     if constexpr (D < 32) {  // (not launched: screen_ok needs d >= 32) rule nothing out
       lflag[lane] = 1u;
@@ -770,21 +777,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
           const sh16x8 fb = *reinterpret_cast<const sh16x8*>(lrow + (tc * 32u + r32) * STH + 16 * ks + k8);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
         }
-        const uint32_t C = tc * 32u + r32;
-        const float ic = linv[C];
-        float4 irv[4];  // rows tr*32 + 8j + 4h + (0..3)
+        const uint32_t C = tc * 32u + r32, hb = 4u * (lane >> 5);
+        const float ic = linv[C], kc = a2 * ic;
+        float4 irv[4], srv[4];  // rows tr*32 + 8j + hb + (0..3)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          irv[j] = *reinterpret_cast<const float4*>(linv + tr * 32u + 8u * (uint32_t)j + 4u * (lane >> 5));
-        bool fail = false;
+        for (int j = 0; j < 4; ++j) {
+          irv[j] = *reinterpret_cast<const float4*>(linv + tr * 32u + 8u * (uint32_t)j + hb);
+          srv[j] = *reinterpret_cast<const float4*>(lsrow + tr * 32u + 8u * (uint32_t)j + hb);
+        }
+        // the lane's pairs (one run per tested tile): rows the image carries, column too, and
+        // R < C on a diagonal tile (local row (q&3) + 8(q>>2) + hb below r32)
+        uint32_t pm = rows16((uint32_t)(vmask >> (tr * 32u + hb)));
+        if (tr == tc) {
+          const uint32_t lim = r32 > hb ? r32 - hb : 0u;
+          pm &= rows16(lim >= 32u ? 0xFFFFFFFFu : ((1u << lim) - 1u));
+        }
+        if (!((vmask >> C) & 1ull)) pm = 0u;
+        uint32_t fm = 0u;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const float4 v = irv[q >> 2];
+          const float4 v = irv[q >> 2], u = srv[q >> 2];
           const float ir = (q & 3) == 0 ? v.x : (q & 3) == 1 ? v.y : (q & 3) == 2 ? v.z : v.w;
-          fail |= test(tr * 32u + (uint32_t)(q & 3) + 8u * (uint32_t)(q >> 2) + 4u * (lane >> 5), C,
-                       acc[q], ir, ic);
+          const float sr = (q & 3) == 0 ? u.x : (q & 3) == 1 ? u.y : (q & 3) == 2 ? u.z : u.w;
+          fm |= test(acc[q], ir, sr, ic, kc) ? (1u << q) : 0u;
         }
-        if (fail) lflag[C >> lg] = 1u;
+        if (fm & pm) lflag[C >> lg] = 1u;
       }
     } else {
       const uint32_t r16 = lane & 15u, k8 = 8u * (lane >> 4);
@@ -796,14 +813,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_
           const sh16x8 f = *reinterpret_cast<const sh16x8*>(lrow + (16u * tb + r16) * STH + 32 * ks + k8);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(f, f, acc, 0, 0, 0);
         }
-        const uint32_t C = 16u * tb + r16;
-        const float ic = linv[C];
-        const float4 v = *reinterpret_cast<const float4*>(linv + 16u * tb + 4u * (lane >> 4));
-        const float irq[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t C = 16u * tb + r16, rb = 16u * tb + 4u * (lane >> 4);
+        const float ic = linv[C], kc = a2 * ic;
+        const float4 v = *reinterpret_cast<const float4*>(linv + rb);
+        const float4 u = *reinterpret_cast<const float4*>(lsrow + rb);
+        const float irq[4] = {v.x, v.y, v.z, v.w}, srq[4] = {u.x, u.y, u.z, u.w};
         bool fail = false;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          fail |= test(16u * tb + 4u * (lane >> 4) + (uint32_t)q, C, acc[q], irq[q], ic);
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t R = rb + (uint32_t)q;
+          const bool pair = (R < C) & ((R >> lg) == (C >> lg)) & (((vmask >> R) & (vmask >> C) & 1ull) != 0ull);
+          fail |= pair & test(acc[q], irq[q], srq[q], ic, kc);
+        }
         if (fail) lflag[C >> lg] = 1u;
       }
     }
