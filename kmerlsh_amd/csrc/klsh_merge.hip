@@ -1287,17 +1287,29 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
 #ifdef KLSH_MERGE_PROF
   if (t == 0) { tp1 = MPROF_T(); TPROF_ADD(0, tp1 - tp0); TPROF_ADD(4, 1); }
 #endif
-  // 1. low-digit counts (4 keys a thread per round, loads first)
-  for (uint32_t i0 = 0; i0 < m; i0 += 1024u) {
-    uint32_t kk[4];
+  // 1. low-digit counts, in the scatter's layout (wave wv: positions wv*1024 + j*64 + lane of each
+  //    4096-key round), the keys and slots of the first round loaded together: a bucket of one
+  //    round (almost all of them) is read once, the scatter below reuses the registers
+  uint32_t k[kItems], v[kItems];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t i = i0 + (uint32_t)q * 256u + t;
-      kk[q] = kin[base + (i < m ? i : 0u)];
+  for (int j = 0; j < (int)kItems; ++j) {
+    const uint32_t p = wv * kWave + (uint32_t)j * 64u + lane;
+    k[j] = kin[base + (p < m ? p : 0u)];
+    v[j] = vin[base + (p < m ? p : 0u)];
+  }
+#pragma unroll
+  for (int j = 0; j < (int)kItems; ++j)
+    if (wv * kWave + (uint32_t)j * 64u + lane < m) atomicAdd(&cnt[k[j] & MASK], 1u);
+  for (uint32_t r0 = kChunk; r0 < m; r0 += kChunk) {  // (rare) further rounds: keys only
+    uint32_t kk[kItems];
+#pragma unroll
+    for (int j = 0; j < (int)kItems; ++j) {
+      const uint32_t p = r0 + wv * kWave + (uint32_t)j * 64u + lane;
+      kk[j] = kin[base + (p < m ? p : 0u)];
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (i0 + (uint32_t)q * 256u + t < m) atomicAdd(&cnt[kk[q] & MASK], 1u);
+    for (int j = 0; j < (int)kItems; ++j)
+      if (r0 + wv * kWave + (uint32_t)j * 64u + lane < m) atomicAdd(&cnt[kk[j] & MASK], 1u);
   }
   __syncthreads();
 #ifdef KLSH_MERGE_PROF
@@ -1371,12 +1383,14 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
 #endif
   const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   for (uint32_t r0 = 0; r0 < m; r0 += kChunk) {
-    uint32_t k[kItems], v[kItems], lr[kItems];
+    uint32_t lr[kItems];
+    if (m > kChunk) {  // (block-uniform) a bucket of several rounds reloads each round
 #pragma unroll
-    for (int j = 0; j < (int)kItems; ++j) {
-      const uint32_t p = r0 + wv * kWave + (uint32_t)j * 64u + lane;
-      k[j] = kin[base + (p < m ? p : 0u)];
-      v[j] = vin[base + (p < m ? p : 0u)];
+      for (int j = 0; j < (int)kItems; ++j) {
+        const uint32_t p = r0 + wv * kWave + (uint32_t)j * 64u + lane;
+        k[j] = kin[base + (p < m ? p : 0u)];
+        v[j] = vin[base + (p < m ? p : 0u)];
+      }
     }
 #pragma unroll
     for (int j = 0; j < (int)kItems; ++j) {
