@@ -4082,6 +4082,14 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
     return;
   }
   const Fork f(w, s);
+  // The small-run chain (screen + merge: the merge phase's critical path in 146 of C2's 218
+  // multi-launch iterations, rocprofv3 trace) on the main stream: it starts without the fork's
+  // cross-stream wait, and at the join only the aux streams are waited for; the >384-row classes
+  // on aux 2 (C2, one box, interleaved: 203.9 -> 200.8 ms per step).  Not when the previous
+  // iteration had many 385..896-row runs (w.big896_aux, C4): the long walks are the critical
+  // path there and keep the main stream (C4 989 -> 1120 ms with the small chain on it).
+  const bool long_heavy = w.big896_aux != 0u;
+  const hipStream_t s_small = long_heavy ? f.lane(2) : s, s_long = long_heavy ? s : f.lane(2);
   // longest walks first on each stream; the longest runs (few, long walks) on the main stream,
   // concurrent with the auxiliary ones (it waits for them at the join)
   launch_big<D, 384, 256, true>(w, 2, slots, dc, r, ctr, n, f.lane(0));
@@ -4090,8 +4098,8 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   // make the main stream the critical path (C4 1794 -> 1432 ms); with a handful of them (C2)
   // the main stream is the better place (measured 281-285 vs 284-294 ms)
   if (!long896(w, dc, r))
-    launch_big<D, 896, 256, false>(w, 3, slots, dc, r, ctr, n, w.big896_aux ? f.lane(2) : s);
-  launch_huge(w, slots, dc, r, ctr, n, s);
+    launch_big<D, 896, 256, false>(w, 3, slots, dc, r, ctr, n, w.big896_aux ? f.lane(2) : s_long);
+  launch_huge(w, slots, dc, r, ctr, n, s_long);
   // 129..192 rows: two workgroups per CU (62 KB of LDS at d = 64, VGPRs capped at 256 like the
   // 65..128 class), ahead of 65..128 on aux 1
   launch_big<D, 192, 256, true>(w, 1, slots, dc, r, ctr, n, f.lane(1));
@@ -4112,16 +4120,16 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
     // (option small_screen_grid; one-wave workgroups: 2048 → 207.9 / 207.8 vs 3072 → 211.2 /
     // 211.1 ms per C2 step on one box, 1024 → 227–228, 1536 / 2560 within noise of 2048)
     const uint32_t sgrid = w.screen_grid ? std::max(64u, w.screen_grid) : 2048u;
-    k_small_screen<D><<<sgrid, 64, 0, f.lane(2)>>>(w, slots, r, dc.s_star, m0, a2, w.kt);
+    k_small_screen<D><<<sgrid, 64, 0, s_small>>>(w, slots, r, dc.s_star, m0, a2, w.kt);
     MergeWork ws = w;
     ws.screened = 1u;
-    if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
-    k_merge_small<D><<<small_grid(w), 64, 0, f.lane(2)>>>(ws, slots, dc, r, ctr);
+    if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], s_small);
+    k_merge_small<D><<<small_grid(w), 64, 0, s_small>>>(ws, slots, dc, r, ctr);
   } else {
-    if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], f.lane(2));
-    k_merge_small<D><<<small_grid(w), 64, 0, f.lane(2)>>>(w, slots, dc, r, ctr);
+    if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[0], s_small);
+    k_merge_small<D><<<small_grid(w), 64, 0, s_small>>>(w, slots, dc, r, ctr);
   }
-  if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[1], f.lane(2));
+  if (w.small_ev[0]) (void)hipEventRecord(w.small_ev[1], s_small);
 }
 
 template <int RB, int NT, int KC>
