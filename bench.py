@@ -370,13 +370,13 @@ WIDE_NAMES = {
 BF16_DENSE_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
-def kernel_rooflines(config, stats, steps, d, trace, shadow):
+def kernel_rooflines(config, stats, steps, d, trace, shadow, tail_rows=1 << 22):
     """Every kernel class's achieved HBM rate (its algorithmic bytes per launch over its average
     HIP-event launch time); the headline is the class with the largest time per step."""
     register = d in (8, 16, 32, 64)
     # SURVEY.md 8(d) bytes: the projection reads the f32 row (4d), a slot and writes a key.
     # shadow: what it actually reads is the fp16 row image (2d bytes a row; the engine keeps one at
-    # d = 16, 32, 64 and d > 64 with d % 8 == 0 unless option "projection" = 1 / "wide_image" = 0),
+    # d = 16, 32, 64 unless option "projection" = 1),
     # plus the f32 row of the close calls: reported beside it as "image"
     row_bytes = 4 * d
     kern = {c: {f: sum(s["kern"][c][f] for s in stats) for f in ("ms", "launches", "rows", "runs")}
@@ -400,8 +400,7 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
         ach = (b / k["launches"]) / (avg * 1e-3) / 1e9
         name = (KERNEL_NAMES if register or c not in WIDE_NAMES else WIDE_NAMES)[c].format(d=d)
         if c == "project" and shadow:
-            name = (f"k_project_h16<{d}>" if register
-                    else "k_project_h16_wide + k_project_fix (span)")
+            name = f"k_project_h16<{d}>"
         if c == "huge" and d in (16, 32):
             name = f"k_merge_long<{d}>"
         pmc = pmc_traffic(config, c) or pmc_traffic(config, {"project": "k_project",
@@ -492,20 +491,22 @@ def kernel_rooflines(config, stats, steps, d, trace, shadow):
     head = dict(max(alone, key=lambda e: e["ms_per_step"]))
     head["kernels"] = sorted(out, key=lambda e: -e["ms_per_step"])
     # The merge PHASE of the iterations whose classes run as separate concurrent launches
-    # (N_t >= 2^20 at the register widths, every iteration at d > 64): first workgroup start of any
+    # (N_t >= tail_rows, the engine's "tail_merge_rows", at the register widths; every iteration
+    # at d > 64): first workgroup start of any
     # merge class to the last end, per iteration (KLSH_K_MERGE stamps), against SURVEY.md 8(d)'s
     # merge share of B_t: N_t x 4d (every row read for the in-bucket merge) + M_t x (4d + 8) (the
     # new row and a member link per merge), summed over those iterations.
     if merge_phase and merge_phase["launches"]:
         tr = np.asarray(trace, dtype=np.float64)
         nxt = np.append(tr[1:], float(stats[-1]["n_final"]))
-        sel = tr >= (1 << 20) if register else tr >= 0
+        sel = tr >= tail_rows if register else tr >= 0
         mb = float((tr[sel] * 4 * d + (tr[sel] - nxt[sel]) * (4 * d + 8)).sum())
         ms = merge_phase["ms"] / steps
         n_it = merge_phase["launches"] / steps
         ach = mb / (ms * 1e-3) / 1e9
         head["phases"] = [{
-            "phase": "merge wall of the multi-launch iterations" + (" (N_t >= 2^20)" if register else ""),
+            "phase": "merge wall of the multi-launch iterations" +
+                     (f" (N_t >= {tail_rows})" if register else ""),
             "iterations_per_step": n_it, "ms_per_step": ms, "bytes_per_step": mb,
             "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 5),
@@ -595,13 +596,13 @@ def main():
         phases[c] = sum(s["kern"][c]["ms"] for s in stats) / args.steps
     # Kernel rooflines.  The projection: algorithmic bytes per launch = rows x
     # (4d row + 4 slot + 4 key).  The small-run merge (runs of 2..64 rows; its own launch in the
-    # iterations of >= 2^20 positions, ~83 ms of a C2 step, timed by HIP events on its stream):
+    # iterations of >= tail_merge_rows positions, timed by HIP events on its stream):
     # rows x (4d row + 4 slot) + merges x (4d new row + 20 metadata: norm, count, head, member
     # link, the removed row's count) — merges counted over the whole iteration (~97 % of them are
     # small-run merges on C2).  The bench line's "roofline" is the one with the larger time per step.
     roofline = kernel_rooflines(args.config, stats, args.steps, d, trace,
-                                bool(eng.get_option("fp16_image")) and
-                                (d <= 64 or bool(eng.get_option("wide_projection"))))
+                                bool(eng.get_option("fp16_image")) and d <= 64,
+                                eng.get_option("tail_merge_rows"))
     # the whole loop against HBM, SURVEY.md §8(d): B_t = N_t (8d + 16) + M_t (4d + 8) bytes per
     # iteration (rows read by the projection and by the merge, keys and order written and read;
     # per merge the new row and a member link), summed over the timed steps

@@ -180,14 +180,13 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *   "small_screen"     1 = runs of 2..64 rows are screened on the fp16 row image first and only
  *                      the ones the screen cannot rule out are merged on the f32 rows
  *   "tail_merge_rows"  iterations below this many rows merge every class in one launch (default
- *                      2^20; tests lower it to reach the per-class launches at small sizes)
+ *                      2^22, at most 2^26; tests lower it to reach the per-class launches at
+ *                      small sizes).  Iterations below min(this, 2^20) rows are also queued
+ *                      several at a time (one host sync per batch)
  *   "h16_segcap" (tests) caps the fp16 projection's per-workgroup fix-up segment.
- *   "wide_image"       1 = keep the fp16 row image for d > 64 too (d % 8 == 0): the wide
- *                      projection reads it (k_project_h16_wide); 0 (default) = the f32 rows
  *   "long_runs"        4 (default) = runs over 384 rows at d = 16 / 32 through k_merge_long
  *                      (Gram bit matrix + one walk step per merge); 1 = only runs over 896 rows;
  *                      0 = k_merge_huge for those
- *   "wide_projection"  1 = wide rows projected from the fp16 image (needs wide_image = 1)
  *   "wide_unrolled"    1 (default) = d = 512 projected by the unrolled screen; 0 = the generic one
  *   "wide_gram"        at d = 512 the group merges of runs of at least this many rows (8, 16, 32
  *                      or 64; default 32) take their decisions from an MFMA Gram matrix with a
@@ -196,7 +195,7 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
 int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value);
 /* Any option above, plus read-only diagnostics: "fp16_image" (1 = the loaded rows have the fp16
  * image), "last_hash_kernel" (klsh_hash_keys' projection kernel: 0 packed chains, 1 fp16-image
- * screen, 2 f32 fp16x3 wide-row screen, 3 fp16-image wide-row screen, -1 none) and
+ * screen, 2 f32 fp16x3 wide-row screen, -1 none) and
  * "last_hash_close_pairs" (its (row, hyperplane) pairs settled by the exact chains). */
 int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value);
 

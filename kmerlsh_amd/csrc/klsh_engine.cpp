@@ -182,9 +182,8 @@ struct klsh_ctx {
   // option "projection" asks for the exact packed chains; every row store of the merge kernels
   // writes it too (store_row4 / store_row1)
   uint16_t* xh_alloc = nullptr;
-  bool wide_image = false;  // option "wide_image": the image for d > 64 too (k_project_h16_wide)
   bool shadow_wanted(int d_) const {
-    return pw.variant != klsh::kProjPacked && klsh::shadow_width_ok(d_) && (d_ <= 64 || wide_image);
+    return pw.variant != klsh::kProjPacked && klsh::shadow_width_ok(d_);
   }
   // Queued tail batches (run_batched; option "tail_batch", default on), their bucket sort as a
   // top-bits pass + the LDS bucket sort that lists the runs (option "tail_local", default on)
@@ -702,11 +701,7 @@ klsh_ctx* klsh_create(int device, int* err) {
   for (auto& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, tflags) == hipSuccess;
   for (auto& e : c->sev) ok = ok && hipEventCreateWithFlags(&e, tflags) == hipSuccess;
   for (int i = 0; i < klsh::kMergeStreams; ++i) {
-#ifdef KLSH_AUX1_HI  // A/B: the 65..192-row stream at the high priority too
-    const bool hi = i <= 1;
-#else
-    const bool hi = i == 0;
-#endif
+    const bool hi = i == 0;  // (the 65..192-row stream high too: measured equal)
     ok = ok && hipStreamCreateWithPriority(&c->mw.aux[i], hipStreamNonBlocking,
                                            (hi && big_prio) ? prio_hi : prio_lo) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&c->mw.join[i], oflags) == hipSuccess;
@@ -1071,7 +1066,9 @@ static int merge_and_compact(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t
 // ring slot and the host reads a chunk's slots when its last sequence number is in — the trace,
 // the RNG counter and the statistics come out exactly as the per-iteration loop's.
 static bool batch_eligible(const klsh_ctx* ctx, uint64_t n, int bucket_thr, int iters_left) {
-  if (!ctx->tail_batch || n < 2 || n >= klsh::tail_merge_max(ctx->mw) || iters_left < 2)
+  // (< 2^20 too: the queued compaction is the one-launch look-back over <= 256 tiles)
+  if (!ctx->tail_batch || n < 2 || n >= std::min<uint64_t>(klsh::tail_merge_max(ctx->mw), 1u << 20) ||
+      iters_left < 2)
     return false;
   if (bucket_thr >= 0 && n > (uint64_t)bucket_thr) return false;
   if (!ctx->zero_copy || !ctx->ring_dev || !ctx->lb.status || ctx->phase_timing) return false;
@@ -1823,11 +1820,6 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->mw.wide_gram = (uint32_t)value;
     return 0;
   }
-  if (n == "wide_projection") {
-    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_projection must be 0 or 1");
-    ctx->pw.wide_h16 = (uint32_t)value;
-    return 0;
-  }
   if (n == "wide_unrolled") {
     if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_unrolled must be 0 or 1");
     ctx->pw.wide_rolled = value ? 0u : 1u;
@@ -1838,12 +1830,6 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->mw.long_off = value == 1 ? 0u : value == 0 ? 1u : 4u;
     KLSH_HIP(hipSetDevice(ctx->device));
     return ctx->cap_slots ? ctx->ensure_long(ctx->cap_slots, ctx->d) : 0;
-  }
-  if (n == "wide_image") {
-    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "wide_image must be 0 or 1");
-    KLSH_HIP(hipSetDevice(ctx->device));
-    ctx->wide_image = value != 0;
-    return ctx->apply_projection_variant();
   }
   if (n == "comm_timeout_s") {
     if (value <= 0) return fail(KLSH_E_ARG, "comm_timeout_s must be > 0");
@@ -1861,7 +1847,7 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   if (n == "wide_group_grid") return grid(&ctx->mw.wide_group_grid);
   if (n == "small_screen_grid") return grid(&ctx->mw.screen_grid);
   if (n == "tail_merge_rows") {
-    if (value < 0 || value > (1 << 20)) return fail(KLSH_E_ARG, "tail_merge_rows must be in [0, 2^20]");
+    if (value < 0 || value > (1 << 26)) return fail(KLSH_E_ARG, "tail_merge_rows must be in [0, 2^26]");
     ctx->mw.tail_max = (uint32_t)value;
     return 0;
   }
@@ -1912,9 +1898,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "tail_screen") *value = ctx->mw.tail_screen;
   else if (n == "tail_screen_grid") *value = ctx->mw.tail_screen_grid;
   else if (n == "tail_big_screen") *value = ctx->mw.tail_big_screen;
-  else if (n == "wide_image") *value = ctx->wide_image;
   else if (n == "long_runs") *value = ctx->mw.long_off == 1u ? 0 : ctx->mw.long_off == 0u ? 1 : ctx->mw.long_off;
-  else if (n == "wide_projection") *value = ctx->pw.wide_h16;
   else if (n == "wide_gram") *value = ctx->mw.wide_gram;
   else if (n == "wide_unrolled") *value = ctx->pw.wide_rolled ? 0 : 1;
   else if (n == "fp16_image") *value = ctx->rows.xh != nullptr;

@@ -116,7 +116,7 @@ struct KTime {
   int phase = -1;  // >= 0: the launch also stamps this phase class (its first start, last end)
 };
 constexpr KTime kNoTime{nullptr, 0, -1, -1};
-// Fold set `t` into the totals and clear it (one workgroup; device code, klsh_device.cuh).
+// Fold set `t` into the totals and clear it (one workgroup; device code, klsh_device.h).
 
 // Merge workspace (device), sized for `cap` positions.
 struct MergeWork {
@@ -179,7 +179,7 @@ struct MergeWork {
   float bs_s_star = 0.0f, bs_m0 = 0.0f, bs_a2 = 0.0f;
   uint32_t tail_screen_grid;  // "tail_screen_grid": its persistent launch there (0: 2048)
   // "tail_merge_rows": below this many positions every merge class runs in ONE launch
-  // (k_merge_tail); 0 = the default 2^20 (tests lower it to reach the per-class launches)
+  // (k_merge_tail); 0 = the default 2^22 (tests lower it to reach the per-class launches)
   uint32_t tail_max;
   hipStream_t aux[3];
   KTime kt;                // per-class stamps of this iteration's merge launches
@@ -190,7 +190,10 @@ struct MergeWork {
 constexpr int kMergeStreams = 3;
 constexpr uint32_t kLongRows = 4096;  // the longest run k_merge_long walks (longer: k_merge_huge)
 inline bool long_ok(int d) { return d == 16 || d == 32; }
-inline uint32_t tail_merge_max(const MergeWork& w) { return w.tail_max ? w.tail_max : (1u << 20); }
+// (2^22 since round 5: with the small-run screen and the big-run prescreen inside it, the one
+// launch beat the four-stream fork/join down to 4M positions — C2, one box, interleaved: 2^20
+// 200.2, 2^21 196.5, 2^22 193.1, 2^23 ~= 2^22, 2^24 +1 ms per step)
+inline uint32_t tail_merge_max(const MergeWork& w) { return w.tail_max ? w.tail_max : (1u << 22); }
 
 // Row state, structure-of-arrays, one entry per slot (a slot is a row of the loaded matrix;
 // a merge writes the consensus into the candidate's slot, cluster.cc:70-74).
@@ -210,9 +213,8 @@ struct Rows {
   uint16_t* xh = nullptr;
 };
 // The fp16 image is kept for these widths (the matrix-core screen takes 16 columns per step).
-// widths that keep the fp16 row image: the register projections' (16, 32, 64) and wide rows whose
-// image rows are 16-B aligned (d > 64, a multiple of 8: k_project_h16_wide)
-inline bool shadow_width_ok(int d) { return d == 16 || d == 32 || d == 64 || (d > 64 && d % 8 == 0); }
+// (the wide-row variants that read an fp16 image of d > 64 rows were measured slower and removed)
+inline bool shadow_width_ok(int d) { return d == 16 || d == 32 || d == 64; }
 
 // The merge test of cluster.cc:68-69 as a threshold on the quotient.  The reference computes
 // sim = dot / (sqrtf(|a|^2) * sqrtf(|b|^2)); dist = 1 - sim; and merges when 1 - dist >= thr.
@@ -248,7 +250,6 @@ struct ProjectWork {
   uint32_t fix_grid;   // "fix_grid": wide-row fix-up workgroups
   uint32_t segcap;     // "h16_segcap" (tests): fix-up entries per fp16-projection workgroup
   uint32_t variant;    // "projection": kProjAuto / kProjPacked / kProjScreen (set per launch)
-  uint32_t wide_h16;   // "wide_projection": 1 = wide rows projected from the fp16 image
   uint32_t wide_rolled;  // "wide_unrolled" = 0: d = 512 through the generic wide screen
 };
 // Projection variants (klsh_set_option "projection"): the default picks the certified
@@ -276,7 +277,7 @@ void launch_project_device_n(const Rows& r, const uint32_t* slots, uint32_t* key
 
 // pw (may be null): the workspace that enables the matrix-core screens (the fp16 row image where
 // r.xh is set, bf16x3 for d > 64).  Returns the kernel it launched (ProjKernel).
-enum ProjKernel : int { kPkNone = -1, kPkPacked = 0, kPkH16 = 1, kPkWide = 2, kPkWideH16 = 3 };
+enum ProjKernel : int { kPkNone = -1, kPkPacked = 0, kPkH16 = 1, kPkWide = 2 };
 int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_t n,
                    const float* W, int h, uint32_t key_or, hipStream_t s,
                    const ProjectWork* pw = nullptr, KTime kt = kNoTime);

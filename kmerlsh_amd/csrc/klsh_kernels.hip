@@ -20,7 +20,7 @@
 #include <string>
 #include <type_traits>
 
-#include "klsh_device.cuh"
+#include "klsh_device.h"
 
 namespace klsh {
 
@@ -90,11 +90,7 @@ __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X,
 #pragma unroll
   for (int r = 0; r < RPL; ++r) {
     const uint32_t pr = p0 + 256u * r;
-#ifdef KLSH_PROJ_IDENT  // diagnostics build only: rows in position order (wrong keys)
-    const float4* src = reinterpret_cast<const float4*>(X + (size_t)(pr < n ? pr : p0) * dp);
-#else
     const float4* src = reinterpret_cast<const float4*>(X + (size_t)slots[pr < n ? pr : p0] * dp);
-#endif
 #pragma unroll
     for (int m = 0; m < D / 4; ++m) {
       const float4 v = src[m];
@@ -138,20 +134,9 @@ __global__ __launch_bounds__(256) void k_project_pk(const float* __restrict__ X,
                  (a[r][c][0].y >= 0.0f ? 4u : 0u) + (a[r][c][1].x >= 0.0f ? 2u : 0u) +
                  (a[r][c][1].y >= 0.0f ? 1u : 0u);
   };
-#ifdef KLSH_PROJ_NOVALU  // diagnostics build only: the row loads without the chains (wrong keys)
-  (void)quads;
-#pragma unroll
-  for (int r = 0; r < RPL; ++r) {
-    float sacc = 0.0f;
-#pragma unroll
-    for (int m = 0; m < D / 2; ++m) sacc += x[r][m].x + x[r][m].y;
-    key[r] = (__float_as_uint(sacc) * 2654435761u) >> (32 - 4 * nq);
-  }
-#else
   int q = 0;
   for (; q + CH <= nq; q += CH) quads(q, std::integral_constant<int, CH>{});
   for (; q < nq; ++q) quads(q, std::integral_constant<int, 1>{});
-#endif
 #pragma unroll
   for (int r = 0; r < RPL; ++r) {
     const uint32_t pr = p0 + 256u * r;
@@ -574,10 +559,9 @@ __device__ __forceinline__ void hsplit8(float4 u, float4 v, wh16x8& hi, wh16x8& 
 
 // DT > 0: d == DT (a multiple of 64), every row load unconditional and the round loop unrolled,
 // so each round waits only for its own loads (vmcnt counts, not vmcnt(0)) and the next round's
-// stay in flight behind the math; KLSH_WIDE_PF rounds are kept ahead (1 or 2).
-#ifndef KLSH_WIDE_PF
-#define KLSH_WIDE_PF 1
-#endif
+// stay in flight behind the math; one round is kept ahead (two measured 2030-2035 vs 1995-2003
+// ms per C5 step).
+constexpr int kWidePF = 1;
 template <int DT>
 __global__ __launch_bounds__(kWideNT, 2) void k_project_mfma_wide(const float* __restrict__ X, int d, int dp,
                                                            const uint32_t* __restrict__ slots,
@@ -640,7 +624,7 @@ __global__ __launch_bounds__(kWideNT, 2) void k_project_mfma_wide(const float* _
       }
     };
     if constexpr (DT > 0) {
-      constexpr int R = DT / 64, PF = KLSH_WIDE_PF, NB = PF + 1;
+      constexpr int R = DT / 64, PF = kWidePF, NB = PF + 1;
       float4 xb[NB][4][2];
       auto load_full = [&](int rd, float4 (&dst)[4][2]) {
 #pragma unroll
@@ -714,146 +698,6 @@ __global__ __launch_bounds__(kWideNT, 2) void k_project_mfma_wide(const float* _
       const float bound = eps * (aab[i] * (1.0f + 0x1p-9f)) + abs_c * (wn + xni) + 0x1p-120f;
       const bool pos = col_ok && sv >= 0.0f;
       // NaN / inf anywhere (S, T or the norms), or |S| within the bound: the exact chain decides
-      const bool am = col_ok && (!(__builtin_fabsf(sv) > bound) || !(xni <= 0x1p60f));
-      const uint64_t bp = __ballot(pos), ba = __ballot(am);
-      const uint32_t r0 = (i & 3) + 8u * (i >> 2);
-      if (lane == r0) {
-        bits = (uint32_t)bp;
-        amb = (uint32_t)ba;
-      }
-      if (lane == r0 + 4u) {
-        bits = (uint32_t)(bp >> 32);
-        amb = (uint32_t)(ba >> 32);
-      }
-    }
-    if (lane < 32 && valid) {
-      keys[row] = (h > 0 ? (__builtin_bitreverse32(bits) >> (32 - h)) : 0u) | key_or;
-      if (amb) {  // to the fix-up list (the exact chains; in place if the list is full)
-        const uint32_t c = (uint32_t)__popc(amb);
-        const uint32_t at = atomicAdd(&pw.ws[0], c);
-        uint32_t a = amb, k = 0;
-        while (a) {
-          const int j = __builtin_ctz(a);
-          a &= a - 1u;
-          if (at + k < pw.cap) {
-            pw.fix[at + k] = make_uint2(row, (uint32_t)j);
-          } else {
-            const float* x = X + (size_t)slots[row] * dp;
-            const float* w = W + (size_t)j * dp;
-            float sd = 0.0f;
-            for (int q = 0; q < d; ++q) sd = sd + w[q] * x[q];
-            const uint32_t bit = 1u << (h - 1 - j);
-            keys[row] = sd >= 0.0f ? (keys[row] | bit) : (keys[row] & ~bit);
-          }
-          ++k;
-        }
-      }
-    }
-  }
-}
-
-// Wide rows from the fp16 row image (d > 64, dp a multiple of 8; the image kept for them too):
-// the same screen as k_project_mfma_wide with x~ = fp16(x) read directly — 2d bytes a row instead
-// of 4d — S = x~.wh + x~.wl (two MFMAs per k-step) and T = |x~|.|wh| (a third).  Against the
-// reference's sequential f32 sum s, per column k: |w_k (x~_k - x_k)| <= 2^-11 |w_k||x_k| (fp16
-// rounding; 2^-25 |w_k| in the subnormal range), the w split and the f32 sums as in k_project_h16,
-// so |S - s| <= h16_eps(d) T' + h16_abs(d) (|w| + |x|) with T' = T (1 + 2^-9) >= sum |w_k||x_k|
-// and |x| taken as 1.001 |x~| + 2^-20.  Close calls, and rows past fp16's range (S or T
-// non-finite), go to the same fix-up list (k_project_fix: the exact chains on the f32 row).
-__global__ __launch_bounds__(kWideNT) void k_project_h16_wide(const uint16_t* __restrict__ XH, int d,
-                                                          int dp, const uint32_t* __restrict__ slots,
-                                                          uint32_t* __restrict__ keys, uint32_t n,
-                                                          const float* __restrict__ X,
-                                                          const float* __restrict__ W, int h,
-                                                          uint32_t key_or, float eps, float abs_c,
-                                                          ProjectWork pw, KTime kt) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
-  kt_fold(kt);
-  kt_begin(kt, KC_PROJECT);
-  const int KS = (d + 15) / 16;
-  wh16x8* bfr = reinterpret_cast<wh16x8*>(psm);  // [KS][64 lanes][hi, lo]
-  float* swn = reinterpret_cast<float*>(psm + (size_t)KS * 64 * 2 * sizeof(wh16x8));  // [32]
-  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, r = lane & 31u, hh = lane >> 5;
-  for (int e = (int)t; e < KS * 64; e += kWideNT) {
-    const int sk = e >> 6, L = e & 63, j = L & 31, k0 = 16 * sk + 8 * (L >> 5);
-    float x[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = (j < h && k0 + q < d) ? W[(size_t)j * dp + k0 + q] : 0.0f;
-    wh16x8 hi, lo;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const _Float16 hb = (_Float16)x[q];
-      hi[q] = hb;
-      lo[q] = (_Float16)(x[q] - (float)hb);
-    }
-    bfr[2 * e] = hi;
-    bfr[2 * e + 1] = lo;
-  }
-  if (t < 32) {
-    float a = 0.0f;
-    for (int k = 0; k < d; ++k) {
-      const float v = (int)t < h ? W[(size_t)t * dp + k] : 0.0f;
-      a += v * v;
-    }
-    swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;
-  }
-  __syncthreads();
-  const float wn = swn[r];
-  const bool col_ok = (int)r < h;
-  constexpr uint32_t NWV = kWideNT / 64;
-  constexpr int R8 = 8;  // k-steps per round of loads (8 x 16 B per lane in flight)
-  const uint32_t step = gridDim.x * NWV * 32u;
-  for (uint32_t g0 = (blockIdx.x * NWV + wv) * 32u; g0 < n; g0 += step) {
-    const uint32_t row = g0 + r;
-    const bool valid = row < n;
-    const uint16_t* xr = XH + (size_t)slots[valid ? row : g0] * dp;
-    pf32x16 acc, aab;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = aab[i] = 0.0f;
-    float ss = 0.0f;
-    uint4 xa[R8], xn8[R8];
-    auto load_round = [&](int s0, uint4 (&dst)[R8]) {
-#pragma unroll
-      for (int q = 0; q < R8; ++q) {
-        const int k0 = 16 * (s0 + q) + 8 * (int)hh;
-        dst[q] = k0 + 8 <= dp ? *reinterpret_cast<const uint4*>(xr + k0) : make_uint4(0u, 0u, 0u, 0u);
-      }
-    };
-    load_round(0, xa);
-    for (int s0 = 0; s0 < KS; s0 += R8) {
-      if (s0 + R8 < KS) load_round(s0 + R8, xn8);
-#pragma unroll
-      for (int q = 0; q < R8; ++q) {
-        if (s0 + q < KS) {  // wave-uniform
-          const wh16x8 ah = __builtin_bit_cast(wh16x8, xa[q]);
-          const wh16x8 aa = __builtin_bit_cast(
-              wh16x8, make_uint4(xa[q].x & 0x7FFF7FFFu, xa[q].y & 0x7FFF7FFFu,
-                                 xa[q].z & 0x7FFF7FFFu, xa[q].w & 0x7FFF7FFFu));
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ss += (float)ah[e] * (float)ah[e];
-          const wh16x8 bh = bfr[2 * ((s0 + q) * 64 + lane)], bl = bfr[2 * ((s0 + q) * 64 + lane) + 1];
-          wh16x8 ba;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ba[e] = __builtin_fabsf16(bh[e]);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
-          aab = __builtin_amdgcn_mfma_f32_32x32x16_f16(aa, ba, aab, 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < R8; ++q) xa[q] = xn8[q];
-    }
-    ss += __shfl_xor(ss, 32, 64);
-    const float xn = __builtin_amdgcn_sqrtf(ss) * 1.001f + 0x1p-20f;
-    uint32_t bits = 0u, amb = 0u;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const uint32_t ri = (i & 3) + 8u * (i >> 2) + 4u * hh;
-      const float xni = __shfl(xn, (int)ri, 64);
-      const float sv = acc[i];
-      const float bound = eps * (aab[i] * (1.0f + 0x1p-9f)) + abs_c * (wn + xni) + 0x1p-120f;
-      const bool pos = col_ok && sv >= 0.0f;
-      // inf in the image (|x| past fp16's range), NaN, |S| within the bound: the exact chain
       const bool am = col_ok && (!(__builtin_fabsf(sv) > bound) || !(xni <= 0x1p60f));
       const uint64_t bp = __ballot(pos), ba = __ballot(am);
       const uint32_t r0 = (i & 3) + 8u * (i >> 2);
@@ -1015,8 +859,6 @@ int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_
                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
           hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_mfma_wide<512>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
-          hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_h16_wide),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
           hipFuncSetAttribute(reinterpret_cast<const void*>(&k_project_fix),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) == hipSuccess;
       (void)lds_ok;
@@ -1029,11 +871,7 @@ int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_
       // stamped as one span: the screen (start) and the fix-up of its close calls (end)
       KTime k1 = kt;
       k1.fold = -1;
-      if (r.xh && pw->wide_h16)  // the fp16 image (option wide_projection; kept: wide_image)
-        k_project_h16_wide<<<gm, dim3(kWideNT), lds, s>>>(r.xh, r.d, r.dp, slots, keys, n, r.x, W,
-                                                          h, key_or, h16_eps(r.d), h16_abs(r.d),
-                                                          *pw, kt);
-      else if (r.d == 512 && !pw->wide_rolled)  // option "wide_unrolled" (default 1)
+      if (r.d == 512 && !pw->wide_rolled)  // option "wide_unrolled" (default 1)
         k_project_mfma_wide<512><<<gm, dim3(kWideNT), lds, s>>>(r.x, r.d, r.dp, slots, keys, n, W,
                                                                 h, key_or, wide_eps(r.d),
                                                                 wide_abs(r.d), *pw, kt);
@@ -1043,7 +881,7 @@ int launch_project(const Rows& r, const uint32_t* slots, uint32_t* keys, uint32_
                                                               *pw, kt);
       const uint32_t fcap = pw->fix_grid ? std::max(16u, pw->fix_grid) : 1024u;  // "fix_grid"
       k_project_fix<<<fcap, block, flds, s>>>(r.x, r.d, r.dp, slots, keys, W, h, *pw, k1);
-      return r.xh && pw->wide_h16 ? kPkWideH16 : kPkWide;
+      return kPkWide;
     }
   }
   if (h16_ok(r, pw) && h > 0) {

@@ -28,7 +28,7 @@
 #include <cstring>
 #include <limits>
 
-#include "klsh_device.cuh"
+#include "klsh_device.h"
 
 namespace klsh {
 
@@ -576,10 +576,6 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
     int c;
     uint32_t bi;
     locate(t, c, bi);
-#ifdef KLSH_SMALL_RT_G
-    if (c == 0) pair_batch<D>(lists[0], n[0], bi, slots, dc, r, ctr, w.dlist);
-    else merge_batch<0, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr, 2u << c);
-#else
     switch (c) {  // wave-uniform
       case 0: pair_batch<D>(lists[0], n[0], bi, slots, dc, r, ctr, w.dlist); break;
       case 1: merge_batch<4, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
@@ -588,7 +584,6 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
       case 4: merge_batch<32, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
       default: merge_batch<64, D>(e.x, e.y, slot, slots, dc, r, lds, w.dlist, ctr); break;
     }
-#endif
     e = e_next;
     slot = slot_next;
   }
@@ -617,16 +612,11 @@ typedef _Float16 sh16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 sh16x2 __attribute__((ext_vector_type(2)));
 typedef float pf16acc __attribute__((ext_vector_type(16)));
 typedef float pf4acc __attribute__((ext_vector_type(4)));
-#ifndef KLSH_SCREEN_AHEAD
-#define KLSH_SCREEN_AHEAD 2
-#endif
-#ifndef KLSH_SCREEN_WPE
-#define KLSH_SCREEN_WPE 2
-#endif
-constexpr int kScreenAhead = KLSH_SCREEN_AHEAD;  // batches whose rows are in flight while one is screened
+// (lookahead 1 / 3 and 3 waves per EU measured the same as 2 / 2)
+constexpr int kScreenAhead = 2;  // batches whose rows are in flight while one is screened
 
 template <int D>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(KLSH_SCREEN_WPE))) void k_small_screen(MergeWork w, const uint32_t* __restrict__ slots,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_small_screen(MergeWork w, const uint32_t* __restrict__ slots,
                                                      Rows r, float s_star, float m0, float a2,
                                                      KTime kt) {
   constexpr int NC = kGroupClasses, STH = D + 8;  // LDS row stride in halves (16-B pad)
@@ -1243,10 +1233,8 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ vout,
                                                     const uint32_t* __restrict__ dtot, int lb,
                                                     int bucket_thr, MergeWork w) {
-#ifndef KLSH_TL_ITEMS
-#define KLSH_TL_ITEMS 16
-#endif
-  constexpr uint32_t kItems = KLSH_TL_ITEMS, kWave = kItems * 64u, kChunk = 4u * kWave;
+  // (4 or 8 keys per lane per round measured the same as 16)
+  constexpr uint32_t kItems = 16, kWave = kItems * 64u, kChunk = 4u * kWave;
   __shared__ uint32_t cnt[1024];      // low-digit counts, then their exclusive starts
   __shared__ uint32_t run_[1024];     // running count of each digit over the rounds
   __shared__ uint32_t wc[4][1024];    // per-wave digit counts of a round, then wave prefixes
@@ -3377,10 +3365,7 @@ constexpr int kWideKC = 64;
 
 // The exact group merges' chunk width (C5: 32 columns halve the staged tile to 9 KB per wave, so
 // LDS no longer caps the waves per CU below what the registers allow)
-#ifndef KLSH_WIDE_EXACT_KC
-#define KLSH_WIDE_EXACT_KC 32
-#endif
-constexpr int kWideXKC = KLSH_WIDE_EXACT_KC;
+constexpr int kWideXKC = 32;
 
 // Columns [c0, c0 + kcp) of the 64 lanes' rows -> LDS rows (stride KC + 4), coalesced:
 // KC/4 lanes per row, 256/KC rows per wave instruction.  kcp is a multiple of 4.
@@ -3618,170 +3603,10 @@ __global__ __launch_bounds__(64) void k_merge_group_wide(const uint2* __restrict
   kt_end(kt, KC_SMALL);
 }
 
-// ---------------------------------------------- the fp16 screen of the small runs, wide rows -----
-// k_small_screen_wide<G>: k_small_screen's certified test (screen_margins) for rows past 64
-// columns (d > 64, d % 8 == 0, with the fp16 image kept: option wide_image), one class per launch
-// as k_merge_group_wide: a wave takes a batch of 64/G runs (lane g = position g), and the Gram
-// blocks of its runs accumulate over 64-column chunks of the fp16 rows staged through LDS (each
-// lane stages its own row's chunk, 8 x 16 B, the next chunk's loads issued before the current
-// chunk's MFMAs).  Runs with a pair it cannot rule out, or a row without a usable fp16 norm, go
-// to w.act[cls] — the only runs k_merge_group_wide then walks on the f32 rows.
-// NCH: 64-column chunks per row at compile time (d = 64 NCH: the chunk loop unrolled, so the
-// next chunk's loads stay in flight across it), 0 = any d (a rolled loop).
-template <int G, int NCH>
-__global__ __launch_bounds__(64) void k_small_screen_wide(const uint2* __restrict__ list, int cls,
-                                                          const uint32_t* __restrict__ slots,
-                                                          Rows r, float s_star, float m0, float a2,
-                                                          MergeWork w, KTime kt) {
-  constexpr int KC = 64, STH = KC + 8;  // halves per staged chunk row, LDS stride (16-B pad)
-  constexpr uint32_t NG = 64 / G;
-  __shared__ __attribute__((aligned(16))) _Float16 lrow[64 * STH];
-  __shared__ float linv[64];
-  __shared__ uint32_t lflag[64];
-  kt_begin(kt, KC_SCREEN);
-  const uint32_t lane = __lane_id();
-  if (blockIdx.x == 0 && lane == 0) w.rc->screened.v = 1u;
-  const uint32_t n = __builtin_amdgcn_readfirstlane(
-      __hip_atomic_load(&w.rc->n_cls[cls].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const uint32_t nb = (n + NG - 1u) / NG;
-  const uint32_t g = lane & (G - 1u), grp = lane / G;
-  constexpr uint32_t lg = (uint32_t)__builtin_ctz(G);
-  const int dp = r.dp, nch = NCH ? NCH : (r.d + KC - 1) / KC;
-  const uint64_t below = lanes_below(lane);
-  for (uint32_t bi = blockIdx.x; bi < nb; bi += gridDim.x) {
-    const uint32_t k = bi * NG + grp;
-    const uint2 e = k < n ? list[k] : make_uint2(0u, 0u);
-    const uint32_t b = e.y;
-    const bool valid = g < b;
-    const uint32_t slot = slots[valid ? e.x + g : e.x];
-    const uint16_t* src = r.xh + (size_t)slot * dp;
-    pf16acc acc[3];
-    pf4acc acc4[4];
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc4[t] = pf4acc{0.0f, 0.0f, 0.0f, 0.0f};
-    float ss = 0.0f;
-    uint4 cur[8], nxt[8];
-    auto load_chunk = [&](int c0, uint4 (&dst)[8]) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int col = c0 + 8 * q;
-        if constexpr (NCH > 0)  // (d = 64 NCH = dp: every load unconditional, so the compiler
-                                // counts them and waits only for the chunk it stages)
-          dst[q] = *reinterpret_cast<const uint4*>(src + col);
-        else
-          dst[q] = valid && col + 8 <= dp ? *reinterpret_cast<const uint4*>(src + col)
-                                          : make_uint4(0u, 0u, 0u, 0u);
-      }
-    };
-    load_chunk(0, cur);
-#pragma unroll
-    for (int ch = 0; ch < (NCH ? NCH : nch); ++ch) {
-      if (ch + 1 < nch) load_chunk((ch + 1) * KC, nxt);
-      wave_lds_fence();  // the previous chunk's tiles are read
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if constexpr (NCH > 0)
-          if (!valid) cur[q] = make_uint4(0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4*>(lrow + lane * STH + 8 * q) = cur[q];
-        const sh16x8 v = __builtin_bit_cast(sh16x8, cur[q]);
-#pragma unroll
-        for (int h2 = 0; h2 < 8; h2 += 2) {
-          const sh16x2 u = {v[h2], v[h2 + 1]};
-          ss = __builtin_amdgcn_fdot2(u, u, ss, false);
-        }
-      }
-      wave_lds_fence();
-      if constexpr (G >= 32) {
-        const uint32_t r32 = lane & 31u, k8 = 8u * (lane >> 5);
-#pragma unroll
-        for (int tt = 0; tt < 3; ++tt) {
-          if (G == 32 && tt == 1) continue;  // two runs: their diagonal tiles only
-          const uint32_t tr = tt == 2 ? 1u : 0u, tc = tt == 0 ? 0u : 1u;
-#pragma unroll
-          for (int ks = 0; ks < KC / 16; ++ks) {
-            const sh16x8 fa = *reinterpret_cast<const sh16x8*>(lrow + (tr * 32u + r32) * STH + 16 * ks + k8);
-            const sh16x8 fb = *reinterpret_cast<const sh16x8*>(lrow + (tc * 32u + r32) * STH + 16 * ks + k8);
-            acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc[tt], 0, 0, 0);
-          }
-        }
-      } else {
-        const uint32_t r16 = lane & 15u, k8 = 8u * (lane >> 4);
-#pragma unroll
-        for (int tb = 0; tb < 4; ++tb)
-#pragma unroll
-          for (int ks = 0; ks < KC / 32; ++ks) {
-            const sh16x8 f = *reinterpret_cast<const sh16x8*>(lrow + (16u * tb + r16) * STH + 32 * ks + k8);
-            acc4[tb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f, f, acc4[tb], 0, 0, 0);
-          }
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
-    }
-    // a row without a usable norm (zero, tiny, fp16 overflow, NaN) keeps its run for the merge
-    const bool bad = valid && !(ss >= 0x1p-100f && ss <= 0x1p100f);
-    linv[lane] = valid && !bad ? 1.0f / __builtin_sqrtf(ss) : 0.0f;
-    lflag[lane] = 0u;
-    wave_lds_fence();
-    if (bad) lflag[lane >> lg] = 1u;
-    const uint64_t vmask = __ballot(valid && !bad);
-    auto test = [&](uint32_t R, uint32_t C, float sv) {
-      if (R < C && (R >> lg) == (C >> lg) && ((vmask >> R) & (vmask >> C) & 1ull)) {
-        const float ir = linv[R], ic = linv[C];
-        const float qv = sv * ir * ic;
-        const float m = m0 + a2 * (ir + ic);
-        if (!(qv < s_star - m)) lflag[R >> lg] = 1u;  // NaN / inf: not ruled out
-      }
-    };
-    if constexpr (G >= 32) {
-      const uint32_t r32 = lane & 31u;
-#pragma unroll
-      for (int tt = 0; tt < 3; ++tt) {
-        if (G == 32 && tt == 1) continue;
-        const uint32_t tr = tt == 2 ? 1u : 0u, tc = tt == 0 ? 0u : 1u;
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-          test(tr * 32u + (uint32_t)(q & 3) + 8u * (uint32_t)(q >> 2) + 4u * (lane >> 5),
-               tc * 32u + r32, acc[tt][q]);
-      }
-    } else {
-      const uint32_t r16 = lane & 15u;
-#pragma unroll
-      for (int tb = 0; tb < 4; ++tb)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          test(16u * tb + 4u * (lane >> 4) + (uint32_t)q, 16u * tb + r16, acc4[tb][q]);
-    }
-    wave_lds_fence();
-    const bool leader = g == 0u && b >= 2u && lflag[lane >> lg] != 0u;
-    const uint64_t lead = __ballot(leader);
-    if (lead) {  // (wave-uniform) the passed runs of the batch to the class's act list
-      const uint32_t first = (uint32_t)__builtin_ctzll(lead);
-      uint32_t base = 0u, rows = leader ? b : 0u;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) rows += (uint32_t)__shfl_xor((int)rows, o, 64);
-      if (lane == first) {
-        base = atomicAdd(&w.rc->n_act[cls].v, (uint32_t)__popcll(lead));
-        atomicAdd(&w.rc->n_act_rows.v, rows);
-      }
-      base = shfl32(base, first);
-      if (leader) w.act[cls][base + (uint32_t)__popcll(lead & below)] = e;
-    }
-    wave_lds_fence();  // (lrow / linv / lflag are rewritten by the next batch)
-  }
-  kt_end(kt, KC_SCREEN);
-}
-
 // Runs of 65..896 rows with wide rows: one workgroup per run, the decision matrix in LDS in
 // position space (as k_merge_big).  A 64x64 decision tile is one wave's job: its 64 rows'
 // chains (one per lane, 64 columns each) run over KC-column chunks, the column block's chunk
 // staged in the wave's own LDS region and read by broadcast.
-#ifndef KLSH_BIGWIDE_GLDS
-#define KLSH_BIGWIDE_GLDS 1
-#endif
 template <int RB, int NT, int KC>
 struct BigWideLayout {
   static constexpr int W = RB / 64;
@@ -3855,7 +3680,7 @@ __global__ __launch_bounds__(NT) void k_merge_big_wide(MergeWork w, int cls,
       for (int k0 = 0; k0 < d; k0 += KC) {
         const int n = min(KC, d - k0), kcp = min(KC, dp - k0);
         lds_fence();
-        if (KLSH_BIGWIDE_GLDS && kcp == KC) {
+        if (kcp == KC) {
           // a full chunk straight into LDS (global_load_lds, 16 B a lane: the tile is unpadded, so
           // instruction i fills floats [256 i, 256 i + 256) lane-linearly) — no registers, every
           // load in flight at once; rows past the run read row c0 (never read back)
@@ -4029,9 +3854,6 @@ static void screen_margins(int d, float* m0, float* a2) {
 static bool screen_ok(const Rows& r, const Decider& dc, const MergeWork& w) {
   return w.small_screen && r.xh && dc.fast && (r.d == 32 || r.d == 64);  // (tiles: d >= 32)
 }
-static bool wide_screen_ok(const Rows& r, const Decider& dc, const MergeWork& w) {
-  return w.small_screen && r.xh && dc.fast && r.d > 64 && r.d % 8 == 0;
-}
 
 // The small-run merge's persistent launch (option "small_grid"; default 12288).
 static uint32_t small_grid(const MergeWork& w) {
@@ -4179,31 +4001,8 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
   // with up to 8192 workgroups; a chain on one stream costs only its kernel boundaries)
   RunCounters* rc = w.rc;
   const hipStream_t sl = f.lane(2);
-  // the fp16 screen first where the image is kept (wide_image): the merges then walk the runs it
-  // could not rule out (w.act)
-  const bool scr = wide_screen_ok(r, dc, w);
-  if (scr) {
-    float m0, a2;
-    screen_margins(r.d, &m0, &a2);
-    auto screen = [&](auto kern, int c, uint32_t per_wave) {
-      kern<<<grid(c, per_wave), 64, 0, sl>>>(w.cls[c], c, slots, r, dc.s_star, m0, a2, w, w.kt);
-    };
-    if (r.d == 512) {  // (C5's width: the chunk loop unrolled)
-      screen(k_small_screen_wide<64, 8>, 5, 1);
-      screen(k_small_screen_wide<32, 8>, 4, 2);
-      screen(k_small_screen_wide<16, 8>, 3, 4);
-      screen(k_small_screen_wide<8, 8>, 2, 8);
-      screen(k_small_screen_wide<4, 8>, 1, 16);
-      screen(k_small_screen_wide<2, 8>, 0, 32);
-    } else {
-      screen(k_small_screen_wide<64, 0>, 5, 1);
-      screen(k_small_screen_wide<32, 0>, 4, 2);
-      screen(k_small_screen_wide<16, 0>, 3, 4);
-      screen(k_small_screen_wide<8, 0>, 2, 8);
-      screen(k_small_screen_wide<4, 0>, 1, 16);
-      screen(k_small_screen_wide<2, 0>, 0, 32);
-    }
-  }
+  // (an fp16-image screen of these runs, k_small_screen_wide, ruled out 96 % of C5's small-run
+  // rows and still cost more than it saved — 2.25 -> 2.78 s per step — and was removed in round 5)
   // runs of 8..64 rows at d = 512 (C5): pairwise decisions on the matrix cores (option
   // wide_gram) with the margin of the bf16x3 Gram value at this width (wide_gram_margin)
   const bool gram = w.wide_gram && dc.fast && r.d == 512;
@@ -4215,9 +4014,8 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
     dg.g_hi = dc.s_star + m;
   }
   auto group = [&](auto kern, int c, uint32_t per_wave, const Decider& dd) {
-    kern<<<grid(c, per_wave), 64, 0, sl>>>(scr ? w.act[c] : w.cls[c],
-                                           scr ? &rc->n_act[c].v : &rc->n_cls[c].v, slots, dd, r,
-                                           ctr, w.dlist, w.kt);
+    kern<<<grid(c, per_wave), 64, 0, sl>>>(w.cls[c], &rc->n_cls[c].v, slots, dd, r, ctr, w.dlist,
+                                           w.kt);
   };
   if (gram && gmin <= 64) group(k_merge_group_wide<64, 512>, 5, 1, dg);
   else group(k_merge_group_wide<64>, 5, 1, dc);

@@ -3,7 +3,7 @@
 // identical.  No arithmetic of the reference lives here — only integer bookkeeping and copies.
 #include <hip/hip_runtime.h>
 
-#include "klsh_device.cuh"
+#include "klsh_device.h"
 
 namespace klsh {
 

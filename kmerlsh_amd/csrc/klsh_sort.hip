@@ -19,7 +19,7 @@
 
 #include <algorithm>
 
-#include "klsh_device.cuh"
+#include "klsh_device.h"
 
 namespace klsh {
 

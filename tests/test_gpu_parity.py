@@ -139,26 +139,24 @@ def adversarial_rows(rng, n, d, w):
     return rows
 
 
-@pytest.mark.parametrize("d,h,wide_image", [(64, 23, 1), (32, 18, 1), (16, 9, 1), (64, 31, 1),
-                                            (32, 1, 1), (8, 7, 1), (512, 20, 1), (512, 20, 0),
-                                            (100, 31, 1), (72, 5, 1), (72, 5, 0), (136, 31, 1)])
-def test_hash_keys_close_calls_vs_oracle(engine, oracle, d, h, wide_image):
-    """The loop's projection kernels (klsh_hash_keys uses the same dispatch and the fp16 row image
-    at d = 16/32/64 and at d > 64 with d % 8 == 0: k_project_h16_wide; wide_image = 0 or
-    d = 100: the f32 fp16x3 screen) on adversarial rows, bit-equal to the reference's sequential
-    chains (hash/lshash.cc:44-59: s == +0/-0 -> 1, tiny negative -> 0, NaN -> 0).  The screen
-    runs and leaves close calls to the exact chains, which the test asserts."""
+@pytest.mark.parametrize("d,h", [(64, 23), (32, 18), (16, 9), (64, 31), (32, 1), (8, 7), (512, 20),
+                                 (100, 31), (72, 5), (136, 31)])
+def test_hash_keys_close_calls_vs_oracle(engine, oracle, d, h):
+    """The loop's projection kernels (klsh_hash_keys uses the same dispatch: the fp16 row image
+    at d = 16/32/64, the f32 fp16x3 screen above 64) on adversarial rows, bit-equal to the
+    reference's sequential chains (hash/lshash.cc:44-59: s == +0/-0 -> 1, tiny negative -> 0,
+    NaN -> 0).  The screen runs and leaves close calls to the exact chains, which the test
+    asserts."""
     from kmerlsh_amd import _native
 
     rng = np.random.default_rng(11 + d + h)
     w, _ = _native.hyperplanes(7 + d, 0, h, d)
     rows = adversarial_rows(rng, 4000, d, w)
-    with options(engine, wide_image=wide_image, wide_projection=wide_image):
-        got = engine.hash_keys(rows, w)
-        kern = engine.get_option("last_hash_kernel")
+    got = engine.hash_keys(rows, w)
+    kern = engine.get_option("last_hash_kernel")
     assert np.array_equal(got, oracle.keys(rows, w)), (d, h)
-    # fp16 screen / packed / f32 fp16x3 wide screen / fp16-image wide screen
-    want = {16: 1, 32: 1, 64: 1, 8: 0}.get(d, 3 if wide_image and d % 8 == 0 else 2)
+    # fp16 screen / packed / f32 fp16x3 wide screen
+    want = {16: 1, 32: 1, 64: 1, 8: 0}.get(d, 2)
     assert kern == want, kern
     if kern:
         assert engine.get_option("last_hash_close_pairs") > 0
@@ -483,28 +481,6 @@ def test_long_runs_in_the_loop_vs_oracle(engine, oracle):
         trace, counter, st = engine.cluster(0.8, 6, 1000000, 41, 4)
         got = engine.result()
     assert st["kern"]["huge"]["launches"] > 0
-    assert np.array_equal(trace, want[3]) and counter == want[4]
-    assert_same_result(got, *want[:3])
-
-
-@pytest.mark.parametrize("d,screen", [(512, 1), (136, 1), (512, 0)])
-def test_wide_small_screen_vs_oracle(engine, oracle, d, screen):
-    """Wide rows with the fp16 image kept (option wide_image): the small runs screened on it
-    first (k_small_screen_wide, one launch per class), only the runs it cannot rule out merged on
-    the f32 rows — same trace, counter and result bits as the oracle, with rows the image cannot
-    carry (fp16 overflow, all-zero image of a nonzero row, zero, NaN)."""
-    rng = np.random.default_rng(d + 3)
-    rows = clustered(rng, 40000, d, 1500, 0.05)
-    rows[5] *= np.float32(1e5)
-    rows[11] *= np.float32(1e-9)
-    rows[13] = 0.0
-    rows[17, 2] = np.nan
-    want = oracle.cluster(rows, 0.8, 5, 1000000, 21, 4)
-    with options(engine, wide_image=1, small_screen=screen, tail_merge_rows=1):
-        engine.load_rows(rows)
-        trace, counter, st = engine.cluster(0.8, 5, 1000000, 21, 4)
-        got = engine.result()
-    assert (st["kern"]["screen"]["launches"] > 0) == bool(screen)
     assert np.array_equal(trace, want[3]) and counter == want[4]
     assert_same_result(got, *want[:3])
 

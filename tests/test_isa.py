@@ -39,8 +39,8 @@ def test_projection_has_no_fused_multiply_add(kernels):
     # d = 8, 16, 32, 64: packed (8 chains, 1 row per lane); the packed wide-row kernel; the generic
     # kernel; the wide-row matrix-core screen (any d, and unrolled for d = 512) + its exact fix-up
     # kernel; the fp16-image screens (d = 16, 32, 64; their close calls settled in the same
-    # kernel); the wide-row fp16-image screen (option wide_projection)
-    assert len(proj) == 13, sorted(proj)
+    # kernel)
+    assert len(proj) == 12, sorted(proj)
     for name, body in proj.items():
         bad = [ln.strip() for ln in body.splitlines() if FMA.match(ln)]
         assert not bad, (name, bad[:5])

@@ -7,7 +7,7 @@
 #include <numeric>
 #include <vector>
 
-#include "klsh_device.cuh"
+#include "klsh_device.h"
 
 namespace klsh {
 struct DstCopyExcl {  // out[i] = exclusive prefix (src read-only)
