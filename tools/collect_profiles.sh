@@ -1,8 +1,10 @@
 #!/bin/bash
 # Round profiles on the GPU box (run through gpurun from the repo root):
-#   C2 bench line, rocprofv3 kernel stats of one C2 step, FETCH_SIZE / WRITE_SIZE of the projection,
-#   the small-run screen and the small-run merge (separate --pmc passes, the engine printing a
-#   progress line every 25 iterations), kernel stats of C4 and C5.  Outputs under gpurun_out/prof/.
+#   C2 bench line, rocprofv3 kernel stats + trace of one C2 step, FETCH_SIZE / WRITE_SIZE of the
+#   kernel classes (projection, sort, runs + k_tail_local, small-run screen, small-run merge,
+#   k_merge_tail, compaction; separate --pmc passes, the engine printing a progress line every 25
+#   iterations), kernel stats of C4 and C5.  Outputs under gpurun_out/prof/; then
+#   python tools/pmc_summary.py <tag> && python tools/check_rooflines.py <tag>
 #   tools/collect_profiles.sh [c2|pmc|c45|all]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -23,9 +25,13 @@ if [ "$1" != pmc ] && [ "$1" != c45 ]; then
   run c2_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/c2_stats -o run -- $B
 fi
 if [ "$1" = pmc ] || [ "$1" = all ]; then
-  for k in k_project k_small_screen k_merge_small; do
-    run c2_fetch_$k 400 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex $k -d $out/c2_fetch_$k -o run -- $B
-    run c2_write_$k 400 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex $k -d $out/c2_write_$k -o run -- $B
+  # class:regex (tools/pmc_summary.py's CLASSES); every pass also collects k_project, whose second
+  # dispatch marks the main loop's start
+  for spec in "project:k_project" "screen:k_small_screen" "small:k_merge_small" "sort:k_sort_" \
+              "tail:k_merge_tail" "runs:k_runs_|k_tail_local" "compact:k_compact"; do
+    c=${spec%%:*}; rx="${spec#*:}|k_project"
+    run c2_fetch_$c 300 rocprofv3 --pmc FETCH_SIZE --output-format csv --kernel-include-regex "$rx" -d $out/c2_fetch_$c -o run -- $B
+    run c2_write_$c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv --kernel-include-regex "$rx" -d $out/c2_write_$c -o run -- $B
   done
 fi
 if [ "$1" = all ] || [ "$1" = c45 ]; then
