@@ -162,11 +162,12 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
     """The reference (oracle/_ref/ref_harness: the reference's own functions, compiled from its
     sources) or the oracle port, timed on this host's cores.
 
-    Default (a bounded sample): one iteration of the loop from its own state at 14 points t in
-    [0, .9 I] (the engine provides the state) at the schedule's threshold for t — the
+    Default (a bounded sample): 3 consecutive iterations of the loop from its own state at 10
+    points t in [0, .9 I] (the engine provides the state) at the schedule's thresholds — the
     harness's iter_w, Cluster()'s loop body through the reference's p_lsh, merge_hashtable,
-    p_cluster / nestedCluster and merge_abundance (Cluster() itself would start at 0.95).  Its
-    per-row cost, interpolated in t and weighted by the loop's N_t trace, estimates T_loop; value
+    p_cluster / nestedCluster and merge_abundance (Cluster() itself would start at 0.95) — the
+    2nd and 3rd timed.  Their per-row cost, interpolated in t and weighted by the loop's N_t
+    trace, estimates T_loop; value
     = N_0 * I / T_loop like the metric.  mode "full": the reference's WHOLE main loop timed once
     (its own Cluster() over all I iterations from the post-init state, ~5 min at C2 on 16
     threads), with the sampled estimate beside it."""
@@ -216,10 +217,14 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
         full = {"value": n0 * iters / secs, "loop_s": secs, "sum_trace": int(sum(sizes[-iters:])),
                 "final_rows": int(re.findall(r"after clustering:\s*(\d+)", out)[-1])}
     trace = np.asarray(trace, dtype=np.float64)
-    # 14 points, densest where N_t and the per-row cost change fastest (the head)
-    ts = sorted({min(iters - 1, int(f * iters))
-                 for f in (0.0, 0.05, 0.1, 0.15, 0.2, 0.25, 0.3, 0.35, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9)})
-    cost, secs_all = [], 0.0
+    # 10 windows, densest where N_t and the per-row cost change fastest (the head).  Each runs 3
+    # consecutive iterations of the loop from the state at t and times the 2nd and 3rd: those run
+    # on the state the reference's own loop left (its allocations, grown member lists), which on
+    # the box costs ~1.4x a state freshly built from arrays (the first iteration of a window).
+    ts = sorted({min(iters - 3, int(f * iters))
+                 for f in (0.0, 0.05, 0.1, 0.15, 0.2, 0.3, 0.4, 0.5, 0.7, 0.9)})
+    step = np.float32((np.float32(0.95) - np.float32(min_sim)) / np.float32(iters))
+    cost, at, secs_all = [], [], 0.0
     for t in ts:
         rows, off, ids = state_at(eng, t, min_sim, iters, counter0)
         n_t = rows.shape[0]
@@ -229,31 +234,41 @@ def cpu_baseline(eng, mode, n0, d, iters, min_sim, counter0, trace):
                 src = write_state(tmp, rows, off, ids)
                 del rows, off, ids
                 out = subprocess.run([harness, "iter_w", src, src + ".off", src + ".ids",
-                                      str(n_t), str(d), repr(thr_t), "1000000"], env=env,
+                                      str(n_t), str(d), repr(thr_t), "1000000", "3",
+                                      repr(float(step))], env=env,
                                      check=True, capture_output=True, text=True,
                                      timeout=900).stdout
-            secs = float(re.findall(r"one iteration takes \(secs\): ([0-9.eE+-]+)", out)[-1])
-        else:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import klsh_oracle
+            it_s = [float(v) for v in re.findall(r"one iteration takes \(secs\): ([0-9.eE+-]+)", out)]
+            it_n = [int(v) for v in re.findall(r"iteration: (\d+) ->", out)]
+            for j in (1, 2):
+                cost.append(it_s[j] / max(1, it_n[j]))
+                at.append(t + j)
+            secs_all += sum(it_s)
+            log(f"cpu baseline ({kind}, {threads} threads): t={t}..{t + 2} N_t={n_t}: "
+                + " / ".join(f"{v:.2f}" for v in it_s) + " s")
+            continue
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import klsh_oracle
 
-            t0 = time.perf_counter()  # (the oracle's one-iteration call runs at 0.95)
-            klsh_oracle.cluster(rows, float(min_sim), 1, 1_000_000, SEED_BASE, 0, off, ids, threads)
-            secs = time.perf_counter() - t0
+        t0 = time.perf_counter()  # (the oracle's one-iteration call runs at 0.95)
+        klsh_oracle.cluster(rows, float(min_sim), 1, 1_000_000, SEED_BASE, 0, off, ids, threads)
+        secs = time.perf_counter() - t0
         log(f"cpu baseline ({kind}, {threads} threads): t={t} N_t={n_t}: {secs:.2f} s")
         secs_all += secs
         cost.append(secs / max(1, n_t))
-    per_row = np.interp(np.arange(len(trace)), ts, cost)
+        at.append(t)
+    per_row = np.interp(np.arange(len(trace)), at, cost)
     t_loop = float((trace * per_row).sum())
     c1 = c1_measured(harness, threads) if kind == "reference" else None
     sampled = {"value": n0 * iters / t_loop, "estimated_loop_s": round(t_loop, 2),
                "sample_seconds": round(secs_all, 2),
-               "sample": (f"one iteration of the main loop from its own state at t = "
-                          f"{', '.join(map(str, ts))} of {iters} ({threads} threads, at the "
-                          f"schedule's threshold for t"
-                          + (", reference harness iter_w" if kind == "reference" else
-                             "; the port's one-iteration call runs at 0.95") +
-                          f"); per-row cost interpolated in t and weighted by the loop's N_t "
+               "sample": ((f"3 consecutive iterations of the main loop from its own state at t = "
+                           f"{', '.join(map(str, ts))} of {iters} ({threads} threads, the "
+                           f"schedule's thresholds, reference harness iter_w), the 2nd and 3rd "
+                           f"timed" if kind == "reference" else
+                           f"one iteration from the state at t = {', '.join(map(str, ts))} of "
+                           f"{iters} (the port's one-iteration call runs at 0.95)") +
+                          f"; per-row cost interpolated in t and weighted by the loop's N_t "
                           f"trace (sum N_t = {int(trace.sum())}) to estimate T_loop")}
     if full:
         return {"value": full["value"], "unit": "k-mers·iterations/s", "cores": threads,

@@ -83,8 +83,8 @@ int main(int argc, char** argv) {
             "  ref_harness cluster ROWS N D MINSIM I BTHR OUTPREFIX\n"
             "  ref_harness cluster_from BINPREFIX D MINSIM I BTHR OUTPREFIX   (input via ReadClusterAll)\n"
             "  ref_harness cluster_w ROWS OFF IDS N D MINSIM I BTHR OUTPREFIX (binary member lists)\n"
-            "  ref_harness iter_w ROWS OFF IDS N D THR BTHR  (ONE iteration of Cluster's body at\n"
-            "                                               threshold THR, timed; no output files)\n"
+            "  ref_harness iter_w ROWS OFF IDS N D THR BTHR [K STEP]  (K (default 1) iterations of\n"
+            "                                               Cluster's body from threshold THR, each timed)\n"
             "  ref_harness convert COUNTS N D VKMERS OUTPREFIX  (uint16 sample-major counts -> convertHTMat)\n"
             "  ref_harness ttest VALUES N M COUNT OUT       (f32 cases of N+M values -> studentttest2,\n"
             "                                               f64 bothtails/lefttail/righttail per case)\n");
@@ -198,8 +198,15 @@ int main(int argc, char** argv) {
       // — Cluster() itself always starts its schedule at 0.95 (:190) — through the reference's
       // own p_lsh, merge_hashtable, p_cluster / nestedCluster and merge_abundance, with the same
       // OpenMP structure, so bench.py can time an iteration of the loop at its scheduled value.
-      const float thr = (float)atof(argv[argi]);
+      // optional K STEP: K consecutive iterations at THR, THR - STEP, ... (the schedule's own
+      // decrement, cluster.cc:330), each timed: the later ones run on the state the loop itself
+      // left (its allocations and member lists), not on one freshly built from arrays
+      const float thr0 = (float)atof(argv[argi]);
       const int bthr = atoi(argv[argi + 1]);
+      const int k_iters = argc > argi + 2 ? std::max(1, atoi(argv[argi + 2])) : 1;
+      const float step = argc > argi + 3 ? (float)atof(argv[argi + 3]) : 0.0f;
+      float thr = thr0;
+      for (int it = 0; it < k_iters; ++it) {
       const size_t n0 = v.size();
       const auto t0 = chrono::high_resolution_clock::now();
       const size_t h = floor(log2(v.size()));
@@ -242,6 +249,9 @@ int main(int argc, char** argv) {
           chrono::duration<double>(chrono::high_resolution_clock::now() - t0).count();
       printf("iteration: %zu -> %zu rows at threshold %.9g, %u threads\n", n0, v.size(), thr, threads);
       printf("one iteration takes (secs): %.6f\n", secs);
+      fflush(stdout);
+      thr -= step;
+      }
       return 0;
     }
     const float min_sim = (float)atof(argv[argi]);

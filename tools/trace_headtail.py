@@ -1,6 +1,7 @@
 """Head / tail split of one C2 step from a rocprofv3 kernel trace: wall time and per-class busy
 time of the iterations with separate merge launches (head) and with k_merge_tail (tail), and the
-head's merge-phase wall.  python tools/trace_headtail.py run_kernel_trace.csv"""
+head's merge-phase wall; with LAST, the last LAST iterations (e.g. C2's 282 below 2^20 rows,
+round 4's "tail") apart.  python tools/trace_headtail.py run_kernel_trace.csv [LAST]"""
 import csv,sys,collections
 rows=list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r:int(r["Start_Timestamp"]))
@@ -12,12 +13,15 @@ for r in rows:
     if cur is not None: cur.append((int(r["Start_Timestamp"]),int(r["End_Timestamp"]),n.split('(')[0].replace('void ','').replace('klsh::','')))
 its=its[1:]
 def cls(n):
-    for k in ["project","sort","runs","merge_tail","merge_small","merge_big","merge_huge","compact"]:
+    for k in ["project","sort","runs","tail_local","small_screen","merge_tail","merge_small","merge_big","merge_huge","merge_long","compact"]:
         if k in n: return k
     return n[:20]
 tail=[i for i,k in enumerate(its) if any('merge_tail' in x[2] for x in k)]
 print("tail iterations",len(tail),"first",tail[0] if tail else None)
-for name,sel in [("head",[i for i in range(len(its)) if i not in set(tail)]),("tail",tail)]:
+last=int(sys.argv[2]) if len(sys.argv)>2 else 0
+groups=[("head",[i for i in range(len(its)) if i not in set(tail)]),("tail",tail)]
+if last: groups+=[("tail-mid",[i for i in tail if i<len(its)-last]),("last%d"%last,list(range(len(its)-last,len(its))))]
+for name,sel in groups:
     tot=0;busy=collections.Counter()
     for i in sel:
         k=its[i]
