@@ -1519,6 +1519,13 @@ __device__ __forceinline__ void gram_decide(uint32_t R, uint32_t C, uint32_t b,
                                             const f32x16 (&acc)[2][2], RowA rowA, RowB rowB,
                                             const float* sq, const Decider& dc, uint64_t* P,
                                             int W, uint32_t* fb) {
+  // d <= 32 (C4's 32-sample rows): tiles with a close call are common enough there that the mask
+  // pass is mostly paid twice -- the lane-by-lane path alone measured C4 992-996 -> 925 ms (one box,
+  // interleaved); at d = 64 the masks win (C2 214 -> 203 ms)
+  if constexpr (D <= 32) {
+    gram_decide_slow<D>(R, C, b, acc, rowA, rowB, sq, dc, P, W, fb);
+    return;
+  }
   const uint32_t lane = __lane_id(), r = lane & 31u, h = lane >> 5;
   const uint32_t a0 = R * 64u, c0 = C * 64u;
   // the norms of my two columns and of my 32 rows (loaded together: one LDS wait)

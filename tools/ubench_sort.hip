@@ -1,5 +1,6 @@
 // Microbenchmark of the bucket sort (klsh_sort.hip) and the device scan.  Build: make -C kmerlsh_amd/csrc ubench; run: tools/ubench_sort N BITS REPS.
 #include <hip/hip_runtime.h>
+#include <hipcub/device/device_radix_sort.hpp>  // reference point only: the library's stable radix sort
 
 #include <algorithm>
 #include <cstdio>
@@ -65,13 +66,42 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, a, b));
     if (r >= 2) sort_ms += ms;
   }
-  // verify
+  // the same sort through hipCUB / rocPRIM (onesweep), timed the same way, checked below
+  float lib_ms = 0;
+  {
+    size_t tb = 0;
+    CK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, n, 0, bits, s));
+    void* tmp;
+    CK(hipMalloc(&tmp, tb));
+    for (int r = 0; r < reps + 2; ++r) {
+      CK(hipMemcpyAsync(k0, kk, 4ull * n, hipMemcpyDeviceToDevice, s));
+      CK(hipMemcpyAsync(v0, vv, 4ull * n, hipMemcpyDeviceToDevice, s));
+      CK(hipEventRecord(a, s));
+      CK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, n, 0, bits, s));
+      CK(hipEventRecord(b, s));
+      CK(hipStreamSynchronize(s));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      if (r >= 2) lib_ms += ms;
+    }
+    CK(hipFree(tmp));
+  }
+  std::vector<uint32_t> lp(n);
+  CK(hipMemcpy(lp.data(), v1, 4ull * n, hipMemcpyDeviceToHost));
+  // verify (our sort ran again so ok/ov hold its output)
+  for (int r = 0; r < 1; ++r) {
+    CK(hipMemcpyAsync(k0, kk, 4ull * n, hipMemcpyDeviceToDevice, s));
+    CK(hipMemcpyAsync(v0, vv, 4ull * n, hipMemcpyDeviceToDevice, s));
+    klsh::radix_sort(k0, v0, k1, v1, n, bits, ws, &ok, &ov, s);
+    CK(hipStreamSynchronize(s));
+  }
   std::vector<uint32_t> gp(n), gk(n);
   CK(hipMemcpy(gp.data(), ov, 4ull * n, hipMemcpyDeviceToHost));
   CK(hipMemcpy(gk.data(), ok, 4ull * n, hipMemcpyDeviceToHost));
   std::vector<uint32_t> want(iota);
   std::stable_sort(want.begin(), want.end(), [&](uint32_t i, uint32_t j) { return keys[i] < keys[j]; });
   const bool sort_ok = gp == want;
+  printf("hipcub SortPairs %s %.1f us\n", lp == want ? "ok" : "BAD", 1e3 * lib_ms / reps);
   // scan: exclusive prefix of the (unsorted) keys into a buffer of its own
   for (int r = 0; r < reps + 2; ++r) {
     CK(hipEventRecord(a, s));
