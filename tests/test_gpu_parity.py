@@ -402,11 +402,14 @@ def test_small_screen_vs_oracle(engine, oracle, d, screen):
     (897, 32, 60, 0.05, 0.9), (1000, 16, 1000, 0.3, 0.99), (1536, 32, 100, 0.05, 0.9),
     (1537, 32, 100, 0.05, 0.9), (2048, 16, 150, 0.05, 0.9), (3000, 32, 300, 0.08, 0.85),
     (4096, 32, 50, 0.03, 0.95), (4097, 32, 400, 0.05, 0.9), (2500, 32, 2, 0.01, 0.9),
-    (1800, 16, 1800, 0.5, 0.999), (1300, 32, 20, 0.2, 0.8)])
+    (1800, 16, 1800, 0.5, 0.999), (1300, 32, 20, 0.2, 0.8), (5656, 32, 400, 0.05, 0.9),
+    (8192, 32, 300, 0.05, 0.9), (6000, 16, 4, 0.01, 0.9), (7000, 32, 7000, 0.5, 0.999),
+    (8193, 32, 400, 0.05, 0.9)])
 def test_long_runs_vs_oracle(engine, oracle, b, d, groups, noise, thr):
     """Runs over 896 rows through k_merge_long (d = 16, 32: the Gram bit matrix in memory, one
     walk step per merge; rows past 1536 / 2048 positions read from memory; over 4096 rows:
-    huge_runs in the same launch): merge-dense and merge-sparse, every length boundary."""
+    huge_runs in the same launch, up to C4's longest, 5656): merge-dense and merge-sparse, every
+    length boundary."""
     rng = np.random.default_rng(b * 11 + d)
     rows = clustered(rng, b, d, groups, noise)
     with options(engine, tail_merge_rows=1):  # the per-class launches, not k_merge_tail
