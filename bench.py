@@ -377,7 +377,7 @@ KERNEL_NAMES = {
 }
 WIDE_NAMES = {
     "project": "k_project_mfma_wide + k_project_fix (span)",
-    "small": "k_merge_group_wide<64..2> (chain on one stream, span)",
+    "small": "k_merge_group_wide<64..2> (six launches on four streams, span)",
     "big128": "k_merge_big_wide<128,128,32>", "big192": "k_merge_big_wide<384,256,32>",
     "big384": "k_merge_big_wide<384,256,32>", "big896": "k_merge_big_wide<896,256,16>",
     "huge": "k_merge_huge<0>",

@@ -4004,8 +4004,8 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
   launch_big_wide<896, 256, 16>(w, 3, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_huge(w, slots, dc, r, ctr, n, f.on ? s : f.lane(0));
   launch_big_wide<128, 128, 32>(w, 0, slots, dc, r, ctr, n, f.lane(1));
-  // the small-run classes, largest runs first, as one chain on aux 2 (each class fills the chip
-  // with up to 8192 workgroups; a chain on one stream costs only its kernel boundaries)
+  // the small-run classes (runs of 2..64 rows), each a persistent launch of up to 16384
+  // one-wave workgroups
   RunCounters* rc = w.rc;
   const hipStream_t sl = f.lane(2);
   // (an fp16-image screen of these runs, k_small_screen_wide, ruled out 96 % of C5's small-run
@@ -4020,9 +4020,17 @@ static void launch_groups_wide(const Rows& r, uint32_t* slots, const Decider& dc
     dg.g_lo = dc.s_star - m;
     dg.g_hi = dc.s_star + m;
   }
+  // The six classes on four streams, not one chain (each class's launch ends with a tail of
+  // latency-bound walks that leaves the chip idle, and the classes' register budgets differ, so
+  // two of them share a SIMD's register file): the main stream takes 64 (behind the short
+  // 385..896-row class), aux 0 32 (behind the 129..384-row classes), aux 1 8 and 4 (behind the
+  // 65..128-row class), aux 2 16 and 2.  C5, interleaved on one box: one chain 1896 / 1898 ms,
+  // this 1733 / 1736 (1691 / 1716 on a second box, where two other assignments measured
+  // 1679–1713 ms).  Index: 5 - class (64, 32, 16, 8, 4, 2).
+  const hipStream_t gs[6] = {s, f.lane(0), sl, f.lane(1), f.lane(1), sl};
   auto group = [&](auto kern, int c, uint32_t per_wave, const Decider& dd) {
-    kern<<<grid(c, per_wave), 64, 0, sl>>>(w.cls[c], &rc->n_cls[c].v, slots, dd, r, ctr, w.dlist,
-                                           w.kt);
+    kern<<<grid(c, per_wave), 64, 0, gs[5 - c]>>>(w.cls[c], &rc->n_cls[c].v, slots, dd, r, ctr,
+                                                   w.dlist, w.kt);
   };
   if (gram && gmin <= 64) group(k_merge_group_wide<64, 512>, 5, 1, dg);
   else group(k_merge_group_wide<64>, 5, 1, dc);
