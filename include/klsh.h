@@ -179,6 +179,11 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *   "small_screen_grid" (merge);
  *   "small_screen"     1 = runs of 2..64 rows are screened on the fp16 row image first and only
  *                      the ones the screen cannot rule out are merged on the f32 rows
+ *   "tail_screen"      1 (default) = the fp16 small-run screen also runs in front of the one-launch
+ *                      merge (k_merge_tail), whose small-run waves then walk only the runs it passed
+ *   "tail_big_screen"  1 (default) = there, 65..384-row runs are first screened on the fp16 image
+ *                      in their workgroup; a run with no pair within the margin reads no f32 row
+ *   "tail_screen_grid" workgroups of that screen's persistent launch (0 = 2048)
  *   "tail_merge_rows"  iterations below this many rows merge every class in one launch (default
  *                      2^22, at most 2^26; tests lower it to reach the per-class launches at
  *                      small sizes).  Iterations below min(this, 2^20) rows are also queued
