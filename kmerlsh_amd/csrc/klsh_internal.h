@@ -299,19 +299,24 @@ void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t 
                   float thr, int bucket_thr, const MergeWork& w, Counters* ctr, hipStream_t s,
                   const uint32_t* n_dev = nullptr, bool runs_ready = false);
 
-// Small iterations (< 2^20 positions, keys of 11..20 bits): the stable bucket sort in two steps
-// that also builds the run lists.  radix_sort_top: the stable partition of (k0, v0) by the top 10
-// of `bits` key bits into (k1, v1); returns the top buckets' sizes (1024 words).
-// launch_tail_local: every top bucket of (k1, v1) sorted stably by its low bits-10 bits into
-// (k0, v0), and its runs of 2+ equal keys listed into w (as launch_runs would).
+// Small iterations (< 2^20 positions, keys of 10..19 bits): the stable bucket sort in two steps
+// that also builds the run lists.  radix_sort_top: the stable partition of (k0, v0) by the top
+// kTailTopBits of `bits` key bits into (k1, v1); returns the top buckets' sizes.
+// launch_tail_local: every top bucket of (k1, v1) sorted stably by its low bits - kTailTopBits
+// bits into (k0, v0), and its runs of 2+ equal keys listed into w (as launch_runs would).
 const uint32_t* radix_sort_top(const uint32_t* k0, const uint32_t* v0, uint32_t* k1, uint32_t* v1,
                                uint32_t n, int bits, uint32_t* ws, hipStream_t s, KTime kt,
                                const uint32_t* n_dev);
 void launch_tail_local(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
                        const uint32_t* dtot, int bits, int bucket_thr, const MergeWork& w,
                        hipStream_t s);
+// the top-bits partition's digit width: 9 (512 top buckets of ~1K keys at C2's tail; the local
+// sorts then take up to 10 low bits) measured C2 188.0-188.7 -> 186.1-186.4 ms against 10 (one box,
+// interleaved, three rounds: the run listing 19.8 -> 18.3 ms per step, half the workgroups and
+// half the same-address list-counter adds)
+constexpr int kTailTopBits = 9;
 inline bool tail_local_ok(uint32_t n_max, int bits) {
-  return n_max <= (1u << 20) && bits >= 11 && bits <= 20;
+  return n_max <= (1u << 20) && bits > kTailTopBits && bits <= kTailTopBits + 10;  // (LDS: 2^10)
 }
 
 // Bucket runs of positions [lo, lo + n) of sorted keys (n_dev: the count read on the device, as

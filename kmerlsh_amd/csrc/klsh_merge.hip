@@ -4069,7 +4069,8 @@ void launch_runs(const uint32_t* key, uint32_t lo, uint32_t n, int bucket_thr, c
 void launch_tail_local(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
                        const uint32_t* dtot, int bits, int bucket_thr, const MergeWork& w,
                        hipStream_t s) {
-  k_tail_local<<<1024, 256, 0, s>>>(kin, vin, kout, vout, dtot, bits - 10, bucket_thr, w);
+  k_tail_local<<<1u << kTailTopBits, 256, 0, s>>>(kin, vin, kout, vout, dtot, bits - kTailTopBits,
+                                                   bucket_thr, w);
 }
 
 void launch_merge(const Rows& r, const uint32_t* key, uint32_t* slots, uint32_t lo, uint32_t hi,

@@ -190,8 +190,8 @@ const uint32_t* radix_sort_top(const uint32_t* k0, const uint32_t* v0, uint32_t*
                                uint32_t n, int bits, uint32_t* ws, hipStream_t s, KTime kt,
                                const uint32_t* n_dev) {
   const uint32_t ntiles = (n + kSortTile - 1) / kSortTile;
-  sort_pass<10>(k0, v0, k1, v1, n, bits - 10, ws, s, kt, true, true, n_dev);
-  return ws + (size_t)1024 * ntiles;
+  sort_pass<kTailTopBits>(k0, v0, k1, v1, n, bits - kTailTopBits, ws, s, kt, true, true, n_dev);
+  return ws + ((size_t)1 << kTailTopBits) * ntiles;
 }
 
 // With n_dev the passes are those of `bits` whatever the device count turns out to be: a queued
