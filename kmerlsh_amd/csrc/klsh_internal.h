@@ -313,10 +313,14 @@ void launch_tail_local(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
 // the top-bits partition's digit width: 9 (512 top buckets of ~1K keys at C2's tail; the local
 // sorts then take up to 10 low bits) measured C2 188.0-188.7 -> 186.1-186.4 ms against 10 (one box,
 // interleaved, three rounds: the run listing 19.8 -> 18.3 ms per step, half the workgroups and
-// half the same-address list-counter adds)
+// half the same-address list-counter adds); 8 (256 buckets, up to 11 low bits) measured slower:
+// run listing 18.4 -> 20.7 ms per step
 constexpr int kTailTopBits = 9;
+// the local sorts' digit capacity: the low bits of a 19-bit key (the queued iterations have
+// N < 2^20, so h <= 19), at least 2^10
+constexpr int kTailLowBits = 19 - kTailTopBits > 10 ? 19 - kTailTopBits : 10;
 inline bool tail_local_ok(uint32_t n_max, int bits) {
-  return n_max <= (1u << 20) && bits > kTailTopBits && bits <= kTailTopBits + 10;  // (LDS: 2^10)
+  return n_max <= (1u << 20) && bits > kTailTopBits && bits <= kTailTopBits + kTailLowBits;
 }
 
 // Bucket runs of positions [lo, lo + n) of sorted keys (n_dev: the count read on the device, as

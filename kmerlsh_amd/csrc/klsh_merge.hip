@@ -1235,9 +1235,10 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
                                                     int bucket_thr, MergeWork w) {
   // (4 or 8 keys per lane per round measured the same as 16)
   constexpr uint32_t kItems = 16, kWave = kItems * 64u, kChunk = 4u * kWave;
-  __shared__ uint32_t cnt[1024];      // low-digit counts, then their exclusive starts
-  __shared__ uint32_t run_[1024];     // running count of each digit over the rounds
-  __shared__ uint32_t wc[4][1024];    // per-wave digit counts of a round, then wave prefixes
+  constexpr uint32_t kRad = 1u << kTailLowBits, kPer = kRad / 256u;  // digits per thread
+  __shared__ uint32_t cnt[kRad];      // low-digit counts, then their exclusive starts
+  __shared__ uint32_t run_[kRad];     // running count of each digit over the rounds
+  __shared__ uint32_t wc[4][kRad];    // per-wave digit counts of a round, then wave prefixes
   __shared__ uint32_t lcnt[kRunRows];  // this bucket's list counts, rows, heads
   __shared__ uint32_t lbase[kRunLists];
   __shared__ uint32_t red[4];
@@ -1260,7 +1261,7 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
   if (lane == 0) red[wv] = part;
-  for (uint32_t i = t; i < 1024u; i += 256) {
+  for (uint32_t i = t; i < kRad; i += 256) {
     cnt[i] = 0u;
     run_[i] = 0u;
     wc[0][i] = wc[1][i] = wc[2][i] = wc[3][i] = 0u;
@@ -1304,12 +1305,12 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
   if (t == 0) { const uint64_t x = MPROF_T(); TPROF_ADD(1, x - tp1); tp1 = x; }
 #endif
   // 2. the runs (digits with a count >= 2) per list, and the digit starts
-  uint32_t c4[4], acc = 0, heads = 0, small_rows = 0;
+  uint32_t c4[kPer], acc = 0, heads = 0, small_rows = 0;
   uint32_t lrows[kBigClasses + 1] = {};
-  int l4[4];
+  int l4[kPer];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t dg = t * 4u + (uint32_t)q;
+  for (int q = 0; q < (int)kPer; ++q) {
+    const uint32_t dg = t * kPer + (uint32_t)q;
     c4[q] = dg < RAD ? cnt[dg] : 0u;
     acc += c4[q];
     heads += c4[q] ? 1u : 0u;
@@ -1325,8 +1326,8 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
   uint32_t total;
   uint32_t pre = block_excl_scan_256(acc, &total);  // (syncs: every lcnt add is in)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t dg = t * 4u + (uint32_t)q;
+  for (int q = 0; q < (int)kPer; ++q) {
+    const uint32_t dg = t * kPer + (uint32_t)q;
     if (dg < RAD) cnt[dg] = pre;
     pre += c4[q];
   }
@@ -1352,10 +1353,10 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
   if (t < (uint32_t)kRunLists) lcnt[t] = 0u;  // (reused as the list cursors)
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < (int)kPer; ++q) {
     const int l = l4[q];
     if (l >= 0) {
-      const uint32_t dg = t * 4u + (uint32_t)q;
+      const uint32_t dg = t * kPer + (uint32_t)q;
       const uint32_t at = lbase[l] + atomicAdd(&lcnt[l], 1u);
       const uint2 e = make_uint2(base + cnt[dg], c4[q]);
       if (l < kGroupClasses) w.cls[l][at] = e;
