@@ -216,6 +216,33 @@ def test_tail_local_sort_vs_oracle(engine, oracle, n, d, groups, noise):
         engine.set_option("tail_local", 1)
 
 
+@pytest.mark.parametrize("n,d,groups,noise,with_oracle", [(1500000, 16, 30000, 0.05, True),
+                                                           (2600000, 32, 60000, 0.05, False)])
+def test_mid_local_sort(engine, oracle, n, d, groups, noise, with_oracle):
+    """Iterations of 2^20 .. 2^22 positions (20- and 21-bit keys: the host-driven path with the
+    one-launch merge) then the queued tail, with option tail_local on and off — the same trace,
+    counter and result bits, and the oracle's for the smaller case.  (A top-10-bit partition +
+    LDS bucket sorts for these keys measured slower than the LSD passes, C2 186.5 -> 188.5 ms,
+    and was not kept.)"""
+    rng = np.random.default_rng(n + d)
+    rows = clustered(rng, n, d, groups, noise)
+    got = []
+    try:
+        for local in (1, 0):
+            engine.set_option("tail_local", local)
+            engine.load_rows(rows)
+            trace, counter, _ = engine.cluster(0.8, 3, 1000000, 41, 9)
+            got.append((trace, counter, engine.result()))
+    finally:
+        engine.set_option("tail_local", 1)
+    assert np.array_equal(got[0][0], got[1][0]) and got[0][1] == got[1][1]
+    assert_same_result(got[0][2], *got[1][2])
+    if with_oracle:
+        want = oracle.cluster(rows, 0.8, 3, 1000000, 41, 9)
+        assert np.array_equal(got[0][0], want[3]) and got[0][1] == want[4]
+        assert_same_result(got[0][2], *want[:3])
+
+
 @pytest.mark.parametrize("d", [64, 32])
 def test_cluster_variants_agree(engine, oracle, d):
     """Options that change the launch sequence, not the result: the queued tail batches
