@@ -58,12 +58,14 @@ typedef struct klsh_ctx klsh_ctx;
 #define KLSH_K_BIG384 6   /* 193..384 */
 #define KLSH_K_BIG896 7   /* 385..896 */
 #define KLSH_K_HUGE 8     /* longer runs (k_merge_huge) */
-#define KLSH_K_TAIL 9     /* iterations below 2^20 positions: every merge class in one k_merge_tail */
+#define KLSH_K_TAIL 9     /* iterations below tail_merge_rows positions (default 2^22): every merge
+                             class in one k_merge_tail */
 #define KLSH_K_COMPACT 10 /* survivor compaction (span) */
 #define KLSH_K_SCREEN 11  /* fp16 screen of the runs of 2..64 rows (SMALL then merges the ones left) */
-#define KLSH_K_MERGE 12   /* a phase, not a kernel: the merge launches of each iteration at >= 2^20
-                             positions (every iteration at d > 64) together — first workgroup start
-                             of any merge class to the last end (their concurrent wall) */
+#define KLSH_K_MERGE 12   /* a phase, not a kernel: the merge launches of each iteration at >=
+                             tail_merge_rows positions (default 2^22), and of every iteration at
+                             d > 64, together — first workgroup start of any merge class to the
+                             last end (their concurrent wall) */
 #define KLSH_KCLASSES 13
 typedef struct klsh_kstat {
   double ms;
@@ -185,7 +187,8 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *                      in their workgroup; a run with no pair within the margin reads no f32 row
  *   "tail_screen_grid" workgroups of that screen's persistent launch (0 = 2048)
  *   "tail_merge_rows"  iterations below this many rows merge every class in one launch (default
- *                      2^22, at most 2^26; tests lower it to reach the per-class launches at
+ *                      2^22, at most 2^22 — the largest size its parity is pinned at; tests
+ *                      lower it to reach the per-class launches at
  *                      small sizes).  Iterations below min(this, 2^20) rows are also queued
  *                      several at a time (one host sync per batch)
  *   "h16_segcap" (tests) caps the fp16 projection's per-workgroup fix-up segment.

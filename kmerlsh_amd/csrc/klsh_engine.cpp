@@ -1847,7 +1847,10 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   if (n == "wide_group_grid") return grid(&ctx->mw.wide_group_grid);
   if (n == "small_screen_grid") return grid(&ctx->mw.screen_grid);
   if (n == "tail_merge_rows") {
-    if (value < 0 || value > (1 << 26)) return fail(KLSH_E_ARG, "tail_merge_rows must be in [0, 2^26]");
+    // capped at the largest size the one-launch merge's parity is pinned at (2^22: C2's
+    // iterations of 2^21..2^22 positions, test_mid_local_sort's 2.6M rows); above it, runs over
+    // 896 rows at d = 16 / 32 would walk in huge_runs instead of k_merge_long, which no test covers
+    if (value < 0 || value > (1 << 22)) return fail(KLSH_E_ARG, "tail_merge_rows must be in [0, 2^22]");
     ctx->mw.tail_max = (uint32_t)value;
     return 0;
   }

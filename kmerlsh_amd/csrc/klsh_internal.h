@@ -90,7 +90,8 @@ struct Counters {
 enum KClass : int {
   KC_PROJECT = 0, KC_SORT, KC_RUNS, KC_SMALL, KC_BIG128, KC_BIG192, KC_BIG384, KC_BIG896, KC_HUGE,
   KC_TAIL, KC_COMPACT, KC_SCREEN,
-  KC_MERGE,  // (a phase) the merge launches of an iteration at >= 2^20 positions, all classes
+  KC_MERGE,  // (a phase) the merge launches of an iteration at >= tail_merge_rows positions
+            // (default 2^22; every iteration at d > 64), all classes
   KC_COUNT
 };
 constexpr int kStampSlots = 16;

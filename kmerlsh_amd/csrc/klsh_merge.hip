@@ -2216,7 +2216,12 @@ __device__ __forceinline__ void big_walk_reg(uint32_t p, uint32_t b, uint64_t* P
     bool rewritten = false;
     if (q < size) {
       const uint32_t y = pos2row[q];
-      rewritten = cnt0[y] != cnt[y];  // every merge into a row raises its count
+      // every merge into a row raises its count, and a row's head changes only through a merge
+      // into it (SetConsensus, funcAB.cc:49-71: ids = ids_cur ++ ids_cand, so the candidate's
+      // slot takes the merged-away row's head and the sum of both counts); swap-remove moves a
+      // row's position, never its slot's data.  So "count unchanged" implies "head, norm and row
+      // unchanged" and those slots need no write-back.
+      rewritten = cnt0[y] != cnt[y];
       if (rewritten) {  // the exact sequential norm of the new row (distance.cc:33-34)
         float nv = 0.0f;
 #pragma unroll

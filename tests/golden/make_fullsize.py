@@ -100,10 +100,15 @@ def run_reference(name: str, counts: np.ndarray, cov: np.ndarray) -> dict:
                              "-M", "C", "--only", "--verbose"], env=env, cwd=wd, check=True,
                             capture_output=True, text=True).stdout
         sizes = [int(v) for v in re.findall(r"Size of profilings\D*(\d+)", so)]
+        # the main loop's own timer (function/cluster.cc:335-338: the last "hash+cluster takes"
+        # line is the main Cluster() call, app/kmerLSH.cc:490)
+        loops = [float(v) for v in re.findall(r"hash\+cluster takes \(secs\): ([0-9.eE+-]+)", so)]
         md5 = {fn: file_md5(os.path.join(wd, fn))
                for fn in ("clustering_result.txt", "clustering_result.txt.clust")}
     return {"trace": sizes[-iters:], "init_trace": sizes[:-iters], "md5": md5,
-            "seconds": round(time.time() - t0, 1)}
+            "seconds": round(time.time() - t0, 1),
+            "main_loop_seconds": loops[-1] if loops else None,
+            "host": "build container (8-core Xeon), OMP_THREAD_LIMIT=1 -T 1"}
 
 
 def run(name: str, threads: int, reference: bool = False) -> dict:
