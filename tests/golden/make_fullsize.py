@@ -55,7 +55,7 @@ FULLSIZE = {
     "c1": (100_000, 8, 1, 10, 10, 0.80),
     "c2": (10_000_000, 64, 11, 500, 500, 0.80),
     "c4": (100_000_000, 32, 13, 100, 100, 0.80),
-    "c5": (10_000_000, 512, 17, 500, 100, 0.80),
+    "c5": (10_000_000, 512, 17, 500, 500, 0.80),
 }
 SEED_BASE = 12345
 INIT_BTHR = 100_000     # app/kmerLSH.cc:285,323 (batch_thresh / 1000)
