@@ -577,28 +577,76 @@ __global__ __launch_bounds__(kWideNT, 2) void k_project_mfma_wide(const float* _
   float* swn = reinterpret_cast<float*>(psm + (size_t)KS * 64 * 2 * sizeof(wh16x8));  // [32]
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, r = lane & 31u, hh = lane >> 5;
   // hyperplane fragments: entry (s, L) = W[j = L&31][16s + 8(L>>5) + 0..7], split
-  for (int e = (int)t; e < KS * 64; e += kWideNT) {
-    const int sk = e >> 6, L = e & 63, j = L & 31, k0 = 16 * sk + 8 * (L >> 5);
-    float x[8];
+  if constexpr (DT > 0) {
+    // d = DT: thread t owns entries e = t + 384u, i.e. hyperplane j = t & 31, column half t >> 5
+    // & 1 and k-steps wv + 6u — every load issued before the first is waited for (a loop of
+    // loads under a bounds check waited for each: ~100 us of the launch at C5's late iterations),
+    // and |w_j| summed from the same registers (12 partial sums per hyperplane, added in a fixed
+    // order: a bound, any order will do)
+    constexpr int KSC = DT / 16, NE = (KSC * 64 + kWideNT - 1) / kWideNT;
+    __shared__ float wpart[32][kWideNT / 32];
+    const int j = (int)(t & 31u), half = (int)((t >> 5) & 1u), jc = j < h ? j : 0;
+    float4 wl[NE][2];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = (j < h && k0 + q < d) ? W[(size_t)j * dp + k0 + q] : 0.0f;
-    wh16x8 hi, lo;
+    for (int u = 0; u < NE; ++u) {
+      const int sk = min((int)wv + (int)(kWideNT / 64) * u, KSC - 1);
+      const float* src = W + (size_t)jc * dp + 16 * sk + 8 * half;
+      wl[u][0] = *reinterpret_cast<const float4*>(src);
+      wl[u][1] = *reinterpret_cast<const float4*>(src + 4);
+    }
+    float sq = 0.0f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const _Float16 hb = (_Float16)x[q];
-      hi[q] = hb;
-      lo[q] = (_Float16)(x[q] - (float)hb);
+    for (int u = 0; u < NE; ++u) {
+      const int sk = (int)wv + (int)(kWideNT / 64) * u;
+      if (sk < KSC) {
+        float x[8] = {wl[u][0].x, wl[u][0].y, wl[u][0].z, wl[u][0].w,
+                      wl[u][1].x, wl[u][1].y, wl[u][1].z, wl[u][1].w};
+        wh16x8 hi, lo;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (j >= h) x[q] = 0.0f;
+          const _Float16 hb = (_Float16)x[q];
+          hi[q] = hb;
+          lo[q] = (_Float16)(x[q] - (float)hb);
+          sq += x[q] * x[q];
+        }
+        const int e = sk * 64 + (int)lane;
+        bfr[2 * e] = hi;
+        bfr[2 * e + 1] = lo;
+      }
     }
-    bfr[2 * e] = hi;
-    bfr[2 * e + 1] = lo;
-  }
-  if (t < 32) {
-    float a = 0.0f;
-    for (int k = 0; k < d; ++k) {
-      const float v = (int)t < h ? W[(size_t)t * dp + k] : 0.0f;
-      a += v * v;
+    wpart[j][t >> 5] = sq;
+    __syncthreads();
+    if (t < 32) {
+      float a = 0.0f;
+#pragma unroll
+      for (int q = 0; q < (int)(kWideNT / 32); ++q) a += wpart[t][q];
+      swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;
     }
-    swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;
+  } else {
+    for (int e = (int)t; e < KS * 64; e += kWideNT) {
+      const int sk = e >> 6, L = e & 63, j = L & 31, k0 = 16 * sk + 8 * (L >> 5);
+      float x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x[q] = (j < h && k0 + q < d) ? W[(size_t)j * dp + k0 + q] : 0.0f;
+      wh16x8 hi, lo;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const _Float16 hb = (_Float16)x[q];
+        hi[q] = hb;
+        lo[q] = (_Float16)(x[q] - (float)hb);
+      }
+      bfr[2 * e] = hi;
+      bfr[2 * e + 1] = lo;
+    }
+    if (t < 32) {
+      float a = 0.0f;
+      for (int k = 0; k < d; ++k) {
+        const float v = (int)t < h ? W[(size_t)t * dp + k] : 0.0f;
+        a += v * v;
+      }
+      swn[t] = __builtin_amdgcn_sqrtf(a) * 1.001f;
+    }
   }
   __syncthreads();
   const float wn = swn[r];
@@ -754,8 +802,22 @@ __global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X
     if (woff_dev) W += (size_t)*woff_dev * dp;
   }
   const uint32_t count = min(pw.ws[0], pw.cap);
-  if (blockIdx.x * 256u < count)
-    for (int i = (int)threadIdx.x; i < h * dp; i += 256) fw[i] = W[i];
+  if (blockIdx.x * 256u < count) {
+    // the h hyperplanes into LDS, 16 float4 loads in flight per lane (dp is a multiple of 4):
+    // a loop of one load per round trip was ~80 us of every launch, whatever its pair count
+    const int nv = h * dp / 4;
+    const float4* W4 = reinterpret_cast<const float4*>(W);
+    float4* fw4 = reinterpret_cast<float4*>(fw);
+    constexpr int U = 16;
+    for (int i0 = (int)threadIdx.x; i0 < nv; i0 += 256 * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = W4[min(i0 + 256 * u, nv - 1)];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (i0 + 256 * u < nv) fw4[i0 + 256 * u] = v[u];
+    }
+  }
   __syncthreads();
   for (uint32_t e = blockIdx.x * 256u + threadIdx.x; e < count; e += gridDim.x * 256u) {
     const uint2 f = pw.fix[e];

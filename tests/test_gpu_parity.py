@@ -486,6 +486,50 @@ def test_long_runs_special_rows(engine, oracle, special):
     assert_same_result(got, *oracle.pcluster(rows, 0.9))
 
 
+@pytest.mark.parametrize("b,groups,noise,thr", [
+    (193, 15, 0.05, 0.9), (384, 30, 0.05, 0.95), (384, 384, 0.3, 0.99), (385, 30, 0.05, 0.95),
+    (385, 3, 0.02, 0.9), (640, 640, 0.3, 0.99), (896, 200, 0.05, 0.95), (896, 2, 0.01, 0.9)])
+@pytest.mark.parametrize("per_class", [1, 0])
+def test_big_runs_d64_vs_oracle(engine, oracle, b, groups, noise, thr, per_class):
+    """d = 64 (C2's width) runs at the 193..384 / 385..896 class edges, merge-dense (one group
+    per row at a high threshold: few merges, many decisions near s*) and merge-sparse or dense
+    (few groups), through the per-class launches (k_merge_big<64, 384 / 896>, tail_merge_rows = 1)
+    and through k_merge_tail's big-run workgroups (the default at these sizes)."""
+    rng = np.random.default_rng(b * 17 + groups)
+    rows = clustered(rng, b, 64, groups, noise)
+    with options(engine, tail_merge_rows=1 if per_class else 0):
+        engine.load_rows(rows)
+        engine.pcluster(thr)
+        got = engine.result()
+    assert_same_result(got, *oracle.pcluster(rows, thr))
+
+
+@pytest.mark.parametrize("special", ["nan", "zero", "huge", "tiny"])
+@pytest.mark.parametrize("b", [385, 896])
+def test_big_runs_d64_special_rows(engine, oracle, special, b):
+    """A 385- / 896-row run at d = 64 with a row the Gram pre-screen cannot call (NaN, zero,
+    1e30, 1e-30 scale): the exact chains decide it, in the tiles and in the walk, through both
+    launch paths."""
+    rng = np.random.default_rng(b)
+    rows = clustered(rng, b, 64, 40, 0.05)
+    k = b // 2
+    if special == "nan":
+        rows[k, 3] = np.nan
+    elif special == "zero":
+        rows[k] = 0.0
+    elif special == "huge":
+        rows[k] *= np.float32(1e30)
+    else:
+        rows[k] *= np.float32(1e-30)
+    want = oracle.pcluster(rows, 0.9)
+    for per_class in (1, 0):
+        with options(engine, tail_merge_rows=1 if per_class else 0):
+            engine.load_rows(rows)
+            engine.pcluster(0.9)
+            got = engine.result()
+        assert_same_result(got, *want)
+
+
 @pytest.mark.parametrize("n,groups,noise", [(200000, 100, 0.03), (300000, 120, 0.3)])
 def test_long_runs_many_at_once_vs_oracle(engine, oracle, n, groups, noise):
     """Hundreds of runs over 896 rows in every launch of k_merge_long (one workgroup each, up
