@@ -26,6 +26,21 @@ namespace klsh {
 constexpr uint32_t kSortTile = 4096;  // keys per workgroup (4 waves x 16 items x 64 lanes)
 constexpr int kSortItems = 16;
 
+// The tile of workgroup b among n: consecutive tiles on one XCD.  Workgroups are dealt round-robin
+// over the 8 XCDs (MI355X_MICROARCH.md, dispatch placement: b and b + 8 share one — for speed
+// only, the mapping is a bijection whatever the placement), and a scatter pass writes each digit
+// of a tile as a ~64-B segment right after the previous tile's segment of that digit: with the
+// neighbouring tiles on one XCD those partial lines meet in one L2 instead of eight.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
+#ifdef KLSH_SORT_NO_XCD
+  (void)n;
+  return b;
+#else
+  const uint32_t q = n >> 3, r = n & 7u, x = b & 7u;
+  return x * q + min(x, r) + (b >> 3);
+#endif
+}
+
 template <int B>
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys, uint32_t n,
                                                    int shift, uint32_t ntiles,
@@ -36,8 +51,9 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
   kt_begin(kt, KC_SORT);  // (only the first pass's launch carries kt)
   if (n_dev) n = *n_dev;  // tiles past it count nothing
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
   for (uint32_t d = t; d < RAD; d += 256) c[d] = 0u;
-  const uint32_t base = blockIdx.x * kSortTile + wv * 1024u + lane;
+  const uint32_t base = tile * kSortTile + wv * 1024u + lane;
   uint32_t k[kSortItems];
 #pragma unroll
   for (int j = 0; j < kSortItems; ++j) {
@@ -49,7 +65,7 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
   for (int j = 0; j < kSortItems; ++j)
     if (base + (uint32_t)j * 64u < n) atomicAdd(&c[(k[j] >> shift) & MASK], 1u);
   __syncthreads();
-  for (uint32_t d = t; d < RAD; d += 256) hist[(size_t)d * ntiles + blockIdx.x] = c[d];
+  for (uint32_t d = t; d < RAD; d += 256) hist[(size_t)d * ntiles + tile] = c[d];
 }
 
 // Workgroup d: hist[d][0..ntiles) -> its exclusive prefix over the tiles; dtot[d] = digit total.
@@ -87,7 +103,8 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
   __shared__ uint32_t ls[RAD];     // tile-local start of each digit
   __shared__ uint32_t gb[RAD];     // output position of tile-local entry 0 of each digit
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t T0 = blockIdx.x * kSortTile;
+  const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
+  const uint32_t T0 = tile * kSortTile;
   const uint32_t base = T0 + wv * 1024u + lane;
   for (uint32_t i = t; i < 4u * RAD; i += 256) (&wc[0][0])[i] = 0u;
   uint32_t k[kSortItems], v[kSortItems];
@@ -142,7 +159,7 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
   for (uint32_t q = 0; q < PER; ++q) {
     const uint32_t d = t * PER + q;
     ls[d] = lpre;
-    gb[d] = dpre + hist[(size_t)d * ntiles + blockIdx.x] - lpre;
+    gb[d] = dpre + hist[(size_t)d * ntiles + tile] - lpre;
     lpre += tot[q];
     dpre += dt[q];
   }
