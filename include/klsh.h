@@ -186,6 +186,10 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *   "tail_big_screen"  1 (default) = there, 65..384-row runs are first screened on the fp16 image
  *                      in their workgroup; a run with no pair within the margin reads no f32 row
  *   "tail_screen_grid" workgroups of that screen's persistent launch (0 = 2048)
+ *   "hip_events"       1 = HIP event pairs around the projection and the small-run merge of the
+ *                      host-driven iterations (klsh_stats project_ms / small_ms, cross-checks of
+ *                      the in-kernel stamps); 0 (default): none — a record costs ~9 us of stream
+ *                      time per iteration
  *   "tail_merge_rows"  iterations below this many rows merge every class in one launch (default
  *                      2^22, at most 2^22 — the largest size its parity is pinned at; tests
  *                      lower it to reach the per-class launches at

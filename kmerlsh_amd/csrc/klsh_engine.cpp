@@ -105,6 +105,8 @@ struct klsh_ctx {
   uint64_t kt_iter = 0;
   klsh::LookBack lb{nullptr, 0};  // the one-launch compaction of small iterations
   bool kernel_timing = true;  // option "kernel_timing"
+  bool hip_events = false;    // option "hip_events": HIP event pairs around the projection and
+                              // the small-run merge (cross-checks of the stamps; cost latency)
 
   // sizes
   int d = 0, dp = 0;
@@ -927,8 +929,8 @@ static int merge_main(klsh_ctx* ctx, uint32_t* fk, uint32_t* fv, uint32_t n, flo
   if (timed) KLSH_HIP(hipEventRecord(ctx->ev[2], s));
   // the small-run merge is a launch of its own at >= 2^20 positions (register widths): its HIP
   // events are the headline's cross-check
-  const bool time_small = kt.blk && st && sync && n >= klsh::tail_merge_max(ctx->mw) &&
-                          klsh::project_device_n_ok(ctx->d);
+  const bool time_small = (ctx->hip_events || ctx->phase_timing) && kt.blk && st && sync &&
+                          n >= klsh::tail_merge_max(ctx->mw) && klsh::project_device_n_ok(ctx->d);
   ctx->mw.small_ev[0] = time_small ? ctx->sev[0] : nullptr;
   ctx->mw.small_ev[1] = time_small ? ctx->sev[1] : nullptr;
   ctx->mw.kt = kt;
@@ -1265,8 +1267,11 @@ static int run_single(klsh_ctx* ctx, float& threshold, float sim_step, int it_be
     const uint64_t j = ctx->kt_iter++;  // this iteration's stamp set
     if (queued && ctx->spec_k != k) return fail(KLSH_E_STATE, "queued projection out of step");
     const int e0 = queued ? ctx->spec_ev : 0;
-    // the projection runs alone on the main stream: an event pair times it (beside its stamps)
-    const bool rec = true;
+    // the projection runs alone on the main stream: with option hip_events an event pair times it
+    // (beside its stamps).  Off by default: each record is a marker packet the stream waits on,
+    // ~9 us between the projection and the sort of every host-driven iteration (rocprofv3 trace,
+    // round 6) — the in-kernel stamps time it without one.
+    const bool rec = ctx->hip_events || ctx->phase_timing;
     if (!queued) {
       if (!ctx->ctr_clean) if (int e = ctx->reset_counters()) return e;
       if (rec) KLSH_HIP(hipEventRecord(ctx->ev[e0], s));
@@ -1865,6 +1870,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
     ctx->mw.tail_big_screen = (uint32_t)value;
     return 0;
   }
+  if (n == "hip_events") {
+    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "hip_events must be 0 or 1");
+    ctx->hip_events = value != 0;
+    return 0;
+  }
   if (n == "small_screen") {
     if (value != 0 && value != 1) return fail(KLSH_E_ARG, "small_screen must be 0 or 1");
     ctx->mw.small_screen = (uint32_t)value;
@@ -1898,6 +1908,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "small_screen_grid") *value = ctx->mw.screen_grid;
   else if (n == "tail_merge_rows") *value = klsh::tail_merge_max(ctx->mw);
   else if (n == "small_screen") *value = ctx->mw.small_screen;
+  else if (n == "hip_events") *value = ctx->hip_events ? 1 : 0;
   else if (n == "tail_screen") *value = ctx->mw.tail_screen;
   else if (n == "tail_screen_grid") *value = ctx->mw.tail_screen_grid;
   else if (n == "tail_big_screen") *value = ctx->mw.tail_big_screen;

@@ -6,9 +6,9 @@ bench.py the workload is rebuilt exactly as bench.py's prepare() builds it — k
 (io/ioMatrix.cc:353-408), the init pass (one iteration at 0.95, bucket threshold 1e5;
 app/kmerLSH.cc:323) — and then the main Cluster() loop (app/kmerLSH.cc:490,
 function/cluster.cc:181-340) runs in the oracle (oracle/klsh_oracle.c, pinned bit-for-bit against
-the reference's own outputs by tests/test_oracle_golden.py).  Long configs are pinned on a prefix
-of their loop (the first `run` iterations of the `iters`-iteration threshold schedule,
-klsh_oracle_cluster_prefix).
+the reference's own outputs by tests/test_oracle_golden.py).  Every config is pinned over its
+whole loop (round 6: C5's 500 iterations too; a config can still be pinned on a prefix, the first
+`run` iterations of the `iters`-iteration threshold schedule, klsh_oracle_cluster_prefix).
 
 Stored per config (tests/golden/fullsize_<config>.json): the init-pass trace and survivors, the main
 loop's N_t trace, the rng counter, Σ N_t, the final count, and md5s of the result in canonical

@@ -1,15 +1,18 @@
 """Full-size parity: the gfx950 engine on the exact bench workloads against the oracle's runs.
 
-tests/golden/fullsize_<config>.json holds the oracle's (and, for C1/C2, also the seeded reference
-CLI's) results on the workloads bench.py times — klsh-synth v1 counts, the mode-C conversion, the
-init pass (app/kmerLSH.cc:323), then the main Cluster() loop (app/kmerLSH.cc:490,
-function/cluster.cc:181-340).  C1, C2 and C4 (100M x 32) are pinned over their whole loop (10,
-500 and 100 iterations; the C4 fixture took the oracle 31 min on 6 threads); C5 (10M x 512) over
-the first 100 of its 500 iterations (33 min), and its full loop is checked through
-size-independent properties: N_t non-increasing, the prefix of the full run equal to the pinned
-prefix, member lists partitioning the kept rows, and a bit-identical replay.
+tests/golden/fullsize_<config>.json holds the oracle's results on the workloads bench.py times —
+klsh-synth v1 counts, the mode-C conversion, the init pass (app/kmerLSH.cc:323), then the main
+Cluster() loop (app/kmerLSH.cc:490, function/cluster.cc:181-340) — and, for C1 and C2, the seeded
+reference CLI's own run on the same count files (-T 1; tests/golden/make_fullsize.py --reference:
+its N_t trace and both output files' md5s equal the oracle's, `reference.agrees`).  All four are
+pinned over their whole loop: C1 (10 iterations), C2 (500; the reference CLI took 37 min), C4
+(100M x 32, 100; the oracle 31 min on 6 threads) and C5 (10M x 512, 500; the oracle 33 min on 6
+threads, round 6 — rounds 3-5 pinned its first 100 iterations).  A fixture pinned on a prefix
+only is checked over its whole loop through size-independent properties (N_t non-increasing,
+member lists partitioning the kept rows, a bit-identical replay).
 
-Bar: bit-exact (N_t trace, rng counter, md5 of the fp32 row bits, member offsets and ids).
+Bar: bit-exact (N_t trace, rng counter, md5 of the fp32 row bits, member offsets and ids, and of
+clustering_result.txt / .clust as written — for C1 and C2 the reference CLI's own files).
 """
 import glob
 import hashlib
@@ -67,6 +70,24 @@ def main_loop(eng, fx, stop_after=0):
     return trace, counter, rows, off, ids
 
 
+def written_md5(rows, off, ids):
+    """md5 of clustering_result.txt / .clust as kmerLSH -M C writes them (io/ioMatrix.cc:265-351,
+    clusters with more than 5 members, app/kmerLSH.cc:498-499)."""
+    import tempfile
+
+    from kmerlsh_amd.io import save_binary, save_result
+
+    with tempfile.TemporaryDirectory() as tmp:
+        f = os.path.join(tmp, "clustering_result.txt")
+        save_result(f + ".clust", off, ids)
+        save_binary(f, rows, off)
+        out = {}
+        for fn in ("clustering_result.txt", "clustering_result.txt.clust"):
+            with open(os.path.join(tmp, fn), "rb") as fh:
+                out[fn] = hashlib.md5(fh.read()).hexdigest()
+        return out
+
+
 def assert_pinned(fx, trace, counter, rows, off, ids):
     assert trace.tolist() == fx["trace"]
     assert counter == fx["counter"]
@@ -87,8 +108,11 @@ def test_fullsize_matches_oracle(name):
         pinned = main_loop(eng, fx, 0 if full else fx["run_iterations"])
         assert_pinned(fx, *pinned)
         if full:
-            if "reference" in fx:  # the reference CLI agreed with the oracle on these files
+            if "written_md5" in fx:  # the files the CLI writes from this result (>5 members)
+                assert written_md5(*pinned[2:]) == fx["written_md5"]
+            if "reference" in fx:  # the reference CLI wrote these same files
                 assert fx["reference"]["agrees"]
+                assert fx["reference"]["md5"] == fx["written_md5"]
             return
         # the whole loop at size: properties (and a bit-identical replay)
         trace, counter, rows, off, ids = main_loop(eng, fx)

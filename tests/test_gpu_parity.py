@@ -605,6 +605,34 @@ def test_small_screen_pcluster_special_rows(engine, oracle, b):
         assert_same_result(got, *oracle.pcluster(rows, 0.9)), (b, special)
 
 
+@pytest.mark.parametrize("b", [17, 33, 64])
+@pytest.mark.parametrize("gram", [8, 32])
+def test_wide_gram_close_calls_vs_oracle(engine, oracle, b, gram):
+    """d = 512 runs whose pairwise cosines crowd the threshold (rows = unit center + isotropic
+    noise scaled so E[cos] = thr: about 1 % of the pairs fall inside the certified margin,
+    wide_gram_margin(512) = 1.37e-4), so the Gram tiles' hit / miss masks AND their close-call
+    path (gram_decide_slow, the exact chains) both decide pairs of one tile — the shape that broke
+    a d = 512 parity test when round 5 tried reusing the masks for the close calls.  Special rows
+    (huge, tiny, zero, NaN) in half of the runs; several runs per bucket-free pcluster call."""
+    rng = np.random.default_rng(b * 31 + gram)
+    d, thr = 512, 0.9
+    s = np.sqrt((1.0 / thr - 1.0) / d)
+    for rep in range(4):
+        c = rng.normal(0, 1, size=d)
+        c /= np.linalg.norm(c)
+        rows = (c[None, :] + rng.normal(0, s, size=(b, d))).astype(np.float32)
+        if rep & 1:
+            rows[1] *= np.float32(1e20)
+            rows[2] *= np.float32(1e-20)
+            rows[3] = 0.0
+            rows[4, 7] = np.nan
+        with options(engine, wide_gram=gram, tail_merge_rows=1):
+            engine.load_rows(rows)
+            engine.pcluster(thr)
+            got = engine.result()
+        assert_same_result(got, *oracle.pcluster(rows, thr)), (b, gram, rep)
+
+
 def seq_sim(a, c):
     """The reference's sim for one pair, op by op in fp32 (distance.cc:27-38)."""
     f = np.float32
