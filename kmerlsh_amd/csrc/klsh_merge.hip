@@ -447,6 +447,134 @@ __device__ __forceinline__ void merge_batch(uint32_t p, uint32_t b, uint32_t slo
   (void)nmerged;
 }
 
+// ------------------------------------------------- the fp16 screen of one batch -----
+typedef _Float16 sh16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 sh16x2 __attribute__((ext_vector_type(2)));
+typedef float pf16acc __attribute__((ext_vector_type(16)));
+typedef float pf4acc __attribute__((ext_vector_type(4)));
+
+// The fp16 screen of one batch: 64/G runs of class c (G = 2 << c lanes each, lane g = position g
+// of its run, b = its run's length, x = its fp16 row).  True on the lanes of a run that some pair
+// of which the screen cannot rule out (or that holds a row without a usable norm); false: the run
+// cannot merge.  LDS (this wave's): lrow [64][D + 8] halves, linv / lsrow / lflag [64].
+template <int D>
+__device__ __forceinline__ bool screen_batch(int c, uint32_t b, const sh16x8 (&x)[D / 8],
+                                             _Float16* lrow, float* linv, float* lsrow,
+                                             uint32_t* lflag, float s_star, float m0, float a2) {
+  constexpr int STH = D + 8;  // LDS row stride in halves (16-B pad)
+  const uint32_t lane = __lane_id();
+  const uint32_t G = 2u << c;
+  const uint32_t g = lane & (G - 1);
+  const bool valid = g < b;
+  float ss = 0.0f;
+#pragma unroll
+  for (int q = 0; q < D / 8; ++q) {
+    *reinterpret_cast<sh16x8*>(lrow + lane * STH + 8 * q) = valid ? x[q] : sh16x8{};
+#pragma unroll
+    for (int hi2 = 0; hi2 < 8; hi2 += 2) {
+      const sh16x2 v = {x[q][hi2], x[q][hi2 + 1]};
+      ss = __builtin_amdgcn_fdot2(v, v, ss, false);
+    }
+  }
+  // a row without a usable norm (zero, tiny, fp16 overflow, NaN) cannot be screened: its run
+  // goes to the exact merge
+  const bool bad = valid && !(ss >= 0x1p-100f && ss <= 0x1p100f);
+  const uint32_t lg = (uint32_t)__builtin_ctz(G);  // log2 G
+  const float il = valid && !bad ? 1.0f / __builtin_sqrtf(ss) : 0.0f;
+  linv[lane] = il;
+  lsrow[lane] = s_star - (m0 + a2 * il);
+  lflag[lane] = 0u;
+  wave_lds_fence();
+  if (bad) lflag[lane >> lg] = 1u;
+  const uint64_t vmask = __ballot(valid && !bad);  // rows the Gram test reads
+  // The Gram blocks of the batch's runs on the matrix cores (x~ . x~ exact products, f32 sums):
+  // 32 x 32 tiles for runs of 17..64 rows (the upper-triangular tiles of each run), 16 x 16
+  // diagonal tiles for shorter runs (4 per batch, runs never cross a 16-row block).  A pair
+  // (R < C) of one run that the screen cannot rule out flags the run in LDS.  The tests are
+  // branch-free over per-row terms loaded up front (a load inside each test's branch was a wait
+  // on LDS per entry): a pair is ruled out when G/(|x~a||x~b|) < s* - (m0 + a2 (1/|x~a| +
+  // 1/|x~b|)), evaluated as (G ir) ic < lsrow[R] - a2 ic — the margin's terms summed in another
+  // order, a few ulps of s* against the margin's 1.5x headroom; pair validity is one per-lane
+  // mask per tile, applied once to the tile's failures.
+  auto test = [&](float sv, float ir, float sr, float ic, float kc) -> bool {
+    return !(sv * ir * ic < sr - kc);  // NaN / inf: not ruled out
+  };
+  // bits (q & 3) + 8 (q >> 2) of w -> bit q (the tile rows of a lane, 32 x 32 layout)
+  auto rows16 = [](uint32_t w) -> uint32_t {
+    return (w & 0xFu) | ((w >> 4) & 0xF0u) | ((w >> 8) & 0xF00u) | ((w >> 12) & 0xF000u);
+  };
+  if constexpr (D < 32) {  // (not launched: screen_ok needs d >= 32) rule nothing out
+    lflag[lane] = 1u;
+  } else if (G >= 32u) {
+    const uint32_t r32 = lane & 31u, k8 = 8u * (lane >> 5);
+#pragma unroll 1
+    for (int tt = 0; tt < 3; ++tt) {
+      const uint32_t tr = tt == 2 ? 1u : 0u, tc = tt == 0 ? 0u : 1u;
+      if (G == 32u && tt == 1) continue;  // two runs: their diagonal tiles only
+      pf16acc acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        const sh16x8 fa = *reinterpret_cast<const sh16x8*>(lrow + (tr * 32u + r32) * STH + 16 * ks + k8);
+        const sh16x8 fb = *reinterpret_cast<const sh16x8*>(lrow + (tc * 32u + r32) * STH + 16 * ks + k8);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
+      }
+      const uint32_t C = tc * 32u + r32, hb = 4u * (lane >> 5);
+      const float ic = linv[C], kc = a2 * ic;
+      float4 irv[4], srv[4];  // rows tr*32 + 8j + hb + (0..3)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        irv[j] = *reinterpret_cast<const float4*>(linv + tr * 32u + 8u * (uint32_t)j + hb);
+        srv[j] = *reinterpret_cast<const float4*>(lsrow + tr * 32u + 8u * (uint32_t)j + hb);
+      }
+      // the lane's pairs (one run per tested tile): rows the image carries, column too, and
+      // R < C on a diagonal tile (local row (q&3) + 8(q>>2) + hb below r32)
+      uint32_t pm = rows16((uint32_t)(vmask >> (tr * 32u + hb)));
+      if (tr == tc) {
+        const uint32_t lim = r32 > hb ? r32 - hb : 0u;
+        pm &= rows16(lim >= 32u ? 0xFFFFFFFFu : ((1u << lim) - 1u));
+      }
+      if (!((vmask >> C) & 1ull)) pm = 0u;
+      uint32_t fm = 0u;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float4 v = irv[q >> 2], u = srv[q >> 2];
+        const float ir = (q & 3) == 0 ? v.x : (q & 3) == 1 ? v.y : (q & 3) == 2 ? v.z : v.w;
+        const float sr = (q & 3) == 0 ? u.x : (q & 3) == 1 ? u.y : (q & 3) == 2 ? u.z : u.w;
+        fm |= test(acc[q], ir, sr, ic, kc) ? (1u << q) : 0u;
+      }
+      if (fm & pm) lflag[C >> lg] = 1u;
+    }
+  } else {
+    const uint32_t r16 = lane & 15u, k8 = 8u * (lane >> 4);
+#pragma unroll 1
+    for (int tb = 0; tb < 4; ++tb) {
+      pf4acc acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int ks = 0; ks < D / 32; ++ks) {
+        const sh16x8 f = *reinterpret_cast<const sh16x8*>(lrow + (16u * tb + r16) * STH + 32 * ks + k8);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(f, f, acc, 0, 0, 0);
+      }
+      const uint32_t C = 16u * tb + r16, rb = 16u * tb + 4u * (lane >> 4);
+      const float ic = linv[C], kc = a2 * ic;
+      const float4 v = *reinterpret_cast<const float4*>(linv + rb);
+      const float4 u = *reinterpret_cast<const float4*>(lsrow + rb);
+      const float irq[4] = {v.x, v.y, v.z, v.w}, srq[4] = {u.x, u.y, u.z, u.w};
+      bool fail = false;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t R = rb + (uint32_t)q;
+        const bool pair = (R < C) & ((R >> lg) == (C >> lg)) & (((vmask >> R) & (vmask >> C) & 1ull) != 0ull);
+        fail |= pair & test(acc[q], irq[q], srq[q], ic, kc);
+      }
+      if (fail) lflag[C >> lg] = 1u;
+    }
+  }
+  wave_lds_fence();
+  return lflag[lane >> lg] != 0u;
+}
+
 // ------------------------------------------------- all small-run classes in one launch -----
 // Runs of 2..64 rows of every size class in ONE persistent launch: the batches of all classes
 // (a batch = one wave's 64/G runs of class G; 64 runs of 2 for the pair class) are numbered in
@@ -608,10 +736,6 @@ __device__ __forceinline__ void small_loop(const MergeWork& w, uint32_t* __restr
 // of waiting for one batch at a time.  One wave per workgroup; the batches of every class (64/G
 // runs of G lanes, lane g = position g) in one persistent space, most expensive class first;
 // passed runs collect in LDS per class and go out 32+ at a time (one atomic per flush).
-typedef _Float16 sh16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 sh16x2 __attribute__((ext_vector_type(2)));
-typedef float pf16acc __attribute__((ext_vector_type(16)));
-typedef float pf4acc __attribute__((ext_vector_type(4)));
 // (lookahead 1 / 3 and 3 waves per EU measured the same as 2 / 2)
 constexpr int kScreenAhead = 2;  // batches whose rows are in flight while one is screened
 
@@ -712,114 +836,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const uint32_t G = 2u << c;
     const uint32_t g = lane & (G - 1);
     const uint32_t b = e.y;
-    const bool valid = g < b;
-    float ss = 0.0f;
-#pragma unroll
-    for (int q = 0; q < D / 8; ++q) {
-      *reinterpret_cast<sh16x8*>(lrow + lane * STH + 8 * q) = valid ? x[q] : sh16x8{};
-#pragma unroll
-      for (int hi2 = 0; hi2 < 8; hi2 += 2) {
-        const sh16x2 v = {x[q][hi2], x[q][hi2 + 1]};
-        ss = __builtin_amdgcn_fdot2(v, v, ss, false);
-      }
-    }
-    // a row without a usable norm (zero, tiny, fp16 overflow, NaN) cannot be screened: its run
-    // goes to the exact merge
-    const bool bad = valid && !(ss >= 0x1p-100f && ss <= 0x1p100f);
-    const uint32_t lg = (uint32_t)__builtin_ctz(G);  // log2 G
-    const float il = valid && !bad ? 1.0f / __builtin_sqrtf(ss) : 0.0f;
-    linv[lane] = il;
-    lsrow[lane] = s_star - (m0 + a2 * il);
-    lflag[lane] = 0u;
-    wave_lds_fence();
-    if (bad) lflag[lane >> lg] = 1u;
-    const uint64_t vmask = __ballot(valid && !bad);  // rows the Gram test reads
-    // The Gram blocks of the batch's runs on the matrix cores (x~ . x~ exact products, f32 sums):
-    // 32 x 32 tiles for runs of 17..64 rows (the upper-triangular tiles of each run), 16 x 16
-    // diagonal tiles for shorter runs (4 per batch, runs never cross a 16-row block).  A pair
-    // (R < C) of one run that the screen cannot rule out flags the run in LDS.  The tests are
-    // branch-free over per-row terms loaded up front (a load inside each test's branch was a wait
-    // on LDS per entry): a pair is ruled out when G/(|x~a||x~b|) < s* - (m0 + a2 (1/|x~a| +
-    // 1/|x~b|)), evaluated as (G ir) ic < lsrow[R] - a2 ic — the margin's terms summed in another
-    // order, a few ulps of s* against the margin's 1.5x headroom; pair validity is one per-lane
-    // mask per tile, applied once to the tile's failures.
-    auto test = [&](float sv, float ir, float sr, float ic, float kc) -> bool {
-      return !(sv * ir * ic < sr - kc);  // NaN / inf: not ruled out
-    };
-    // bits (q & 3) + 8 (q >> 2) of w -> bit q (the tile rows of a lane, 32 x 32 layout)
-    auto rows16 = [](uint32_t w) -> uint32_t {
-      return (w & 0xFu) | ((w >> 4) & 0xF0u) | ((w >> 8) & 0xF00u) | ((w >> 12) & 0xF000u);
-    };
-    if constexpr (D < 32) {  // (not launched: screen_ok needs d >= 32) rule nothing out
-      lflag[lane] = 1u;
-    } else if (G >= 32u) {
-      const uint32_t r32 = lane & 31u, k8 = 8u * (lane >> 5);
-#pragma unroll 1
-      for (int tt = 0; tt < 3; ++tt) {
-        const uint32_t tr = tt == 2 ? 1u : 0u, tc = tt == 0 ? 0u : 1u;
-        if (G == 32u && tt == 1) continue;  // two runs: their diagonal tiles only
-        pf16acc acc;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          const sh16x8 fa = *reinterpret_cast<const sh16x8*>(lrow + (tr * 32u + r32) * STH + 16 * ks + k8);
-          const sh16x8 fb = *reinterpret_cast<const sh16x8*>(lrow + (tc * 32u + r32) * STH + 16 * ks + k8);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
-        }
-        const uint32_t C = tc * 32u + r32, hb = 4u * (lane >> 5);
-        const float ic = linv[C], kc = a2 * ic;
-        float4 irv[4], srv[4];  // rows tr*32 + 8j + hb + (0..3)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          irv[j] = *reinterpret_cast<const float4*>(linv + tr * 32u + 8u * (uint32_t)j + hb);
-          srv[j] = *reinterpret_cast<const float4*>(lsrow + tr * 32u + 8u * (uint32_t)j + hb);
-        }
-        // the lane's pairs (one run per tested tile): rows the image carries, column too, and
-        // R < C on a diagonal tile (local row (q&3) + 8(q>>2) + hb below r32)
-        uint32_t pm = rows16((uint32_t)(vmask >> (tr * 32u + hb)));
-        if (tr == tc) {
-          const uint32_t lim = r32 > hb ? r32 - hb : 0u;
-          pm &= rows16(lim >= 32u ? 0xFFFFFFFFu : ((1u << lim) - 1u));
-        }
-        if (!((vmask >> C) & 1ull)) pm = 0u;
-        uint32_t fm = 0u;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const float4 v = irv[q >> 2], u = srv[q >> 2];
-          const float ir = (q & 3) == 0 ? v.x : (q & 3) == 1 ? v.y : (q & 3) == 2 ? v.z : v.w;
-          const float sr = (q & 3) == 0 ? u.x : (q & 3) == 1 ? u.y : (q & 3) == 2 ? u.z : u.w;
-          fm |= test(acc[q], ir, sr, ic, kc) ? (1u << q) : 0u;
-        }
-        if (fm & pm) lflag[C >> lg] = 1u;
-      }
-    } else {
-      const uint32_t r16 = lane & 15u, k8 = 8u * (lane >> 4);
-#pragma unroll 1
-      for (int tb = 0; tb < 4; ++tb) {
-        pf4acc acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int ks = 0; ks < D / 32; ++ks) {
-          const sh16x8 f = *reinterpret_cast<const sh16x8*>(lrow + (16u * tb + r16) * STH + 32 * ks + k8);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(f, f, acc, 0, 0, 0);
-        }
-        const uint32_t C = 16u * tb + r16, rb = 16u * tb + 4u * (lane >> 4);
-        const float ic = linv[C], kc = a2 * ic;
-        const float4 v = *reinterpret_cast<const float4*>(linv + rb);
-        const float4 u = *reinterpret_cast<const float4*>(lsrow + rb);
-        const float irq[4] = {v.x, v.y, v.z, v.w}, srq[4] = {u.x, u.y, u.z, u.w};
-        bool fail = false;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t R = rb + (uint32_t)q;
-          const bool pair = (R < C) & ((R >> lg) == (C >> lg)) & (((vmask >> R) & (vmask >> C) & 1ull) != 0ull);
-          fail |= pair & test(acc[q], irq[q], srq[q], ic, kc);
-        }
-        if (fail) lflag[C >> lg] = 1u;
-      }
-    }
-    wave_lds_fence();
-    const bool grp = lflag[lane >> lg] != 0u;
+    const bool grp = screen_batch<D>(c, b, x, lrow, linv, lsrow, lflag, s_star, m0, a2);
     const bool leader = g == 0u && b >= 2u && grp;
     const uint64_t lead = __ballot(leader);
     if (lead) {
@@ -1218,7 +1235,7 @@ __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, uint32_t n, int
 
 // ------------------------------------------- small iterations: local bucket sort + runs -----
 // Below 2^20 positions the stable bucket order (merge_hashtable, cluster.cc:15-30) is built in two
-// steps: a stable partition by the top 10 key bits (radix_sort_top: one hist / dscan / scatter
+// steps: a stable partition by the top kTailTopBits = 9 key bits (radix_sort_top: one hist / dscan / scatter
 // pass), then this kernel — workgroup d takes top bucket d, a contiguous range of the partition in
 // canonical order, and sorts it stably by the remaining `lb` low bits (a counting sort in LDS:
 // digit counts, their exclusive scan, then ranks among equal digits in position order from wave
@@ -1233,8 +1250,9 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ vout,
                                                     const uint32_t* __restrict__ dtot, int lb,
                                                     int bucket_thr, MergeWork w) {
-  // (4 or 8 keys per lane per round measured the same as 16)
-  constexpr uint32_t kItems = 16, kWave = kItems * 64u, kChunk = 4u * kWave;
+  // (4 or 8 keys per lane per round measured the same as 16; J adaptive vs always 16: C2 run
+  // listing 18.2 vs 18.4 ms per step, one box, three rounds)
+  constexpr uint32_t kItems = 16;  // keys per lane per round at most
   constexpr uint32_t kRad = 1u << kTailLowBits, kPer = kRad / 256u;  // digits per thread
   __shared__ uint32_t cnt[kRad];      // low-digit counts, then their exclusive starts
   __shared__ uint32_t run_[kRad];     // running count of each digit over the rounds
@@ -1276,19 +1294,23 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
 #ifdef KLSH_MERGE_PROF
   if (t == 0) { tp1 = MPROF_T(); TPROF_ADD(0, tp1 - tp0); TPROF_ADD(4, 1); }
 #endif
-  // 1. low-digit counts, in the scatter's layout (wave wv: positions wv*1024 + j*64 + lane of each
-  //    4096-key round), the keys and slots of the first round loaded together: a bucket of one
+  // 1. low-digit counts, in the scatter's layout: a round covers J * 256 positions, wave wv the J*64
+  //    consecutive ones from wv*J*64 (item j of lane l: + j*64 + l), J = ceil(m / 256) up to 16 —
+  //    so a bucket of a few hundred keys is spread over all four waves instead of being wave 0's
+  //    chain of ranks.  The keys and slots of the first round are loaded together: a bucket of one
   //    round (almost all of them) is read once, the scatter below reuses the registers
+  const uint32_t J = min(kItems, (m + 255u) / 256u), kChunk = J * 256u, kWave = J * 64u;
   uint32_t k[kItems], v[kItems];
 #pragma unroll
   for (int j = 0; j < (int)kItems; ++j) {
     const uint32_t p = wv * kWave + (uint32_t)j * 64u + lane;
-    k[j] = kin[base + (p < m ? p : 0u)];
-    v[j] = vin[base + (p < m ? p : 0u)];
+    const bool ok = (uint32_t)j < J && p < m;
+    k[j] = kin[base + (ok ? p : 0u)];
+    v[j] = vin[base + (ok ? p : 0u)];
   }
 #pragma unroll
   for (int j = 0; j < (int)kItems; ++j)
-    if (wv * kWave + (uint32_t)j * 64u + lane < m) atomicAdd(&cnt[k[j] & MASK], 1u);
+    if ((uint32_t)j < J && wv * kWave + (uint32_t)j * 64u + lane < m) atomicAdd(&cnt[k[j] & MASK], 1u);
   for (uint32_t r0 = kChunk; r0 < m; r0 += kChunk) {  // (rare) further rounds: keys only
     uint32_t kk[kItems];
 #pragma unroll
@@ -1365,7 +1387,7 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
       else w.over[at] = e;
     }
   }
-  // 3. the stable scatter, 4096 keys per round (wave wv: positions wv*1024 + j*64 + lane)
+  // 3. the stable scatter, J * 256 keys per round (wave wv: positions wv*J*64 + j*64 + lane)
 #ifdef KLSH_MERGE_PROF
   __syncthreads();
   if (t == 0) { const uint64_t x = MPROF_T(); TPROF_ADD(2, x - tp1); tp1 = x; }
@@ -1383,19 +1405,22 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     }
 #pragma unroll
     for (int j = 0; j < (int)kItems; ++j) {
-      const bool valid = r0 + wv * kWave + (uint32_t)j * 64u + lane < m;
-      const uint32_t dig = k[j] & MASK;
-      uint64_t match = __ballot(valid);
-      for (int b = 0; b < lb; ++b) {
-        const bool bit = (dig >> b) & 1u;
-        const uint64_t mb = __ballot(bit);
-        match &= bit ? mb : ~mb;
+      lr[j] = 0u;
+      if ((uint32_t)j < J) {  // (uniform)
+        const bool valid = r0 + wv * kWave + (uint32_t)j * 64u + lane < m;
+        const uint32_t dig = k[j] & MASK;
+        uint64_t match = __ballot(valid);
+        for (int b = 0; b < lb; ++b) {
+          const bool bit = (dig >> b) & 1u;
+          const uint64_t mb = __ballot(bit);
+          match &= bit ? mb : ~mb;
+        }
+        const uint32_t old = wc[wv][dig];  // every lane reads before the group's leader writes
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (valid && (match & lt) == 0ull) wc[wv][dig] = old + (uint32_t)__popcll(match);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        lr[j] = old + (uint32_t)__popcll(match & lt);
       }
-      const uint32_t old = wc[wv][dig];  // every lane reads before the group's leader writes
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (valid && (match & lt) == 0ull) wc[wv][dig] = old + (uint32_t)__popcll(match);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      lr[j] = old + (uint32_t)__popcll(match & lt);
     }
     __syncthreads();
     for (uint32_t dg = t; dg < RAD; dg += 256) {  // wave prefixes of this round
@@ -1410,7 +1435,7 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < (int)kItems; ++j) {
-      if (r0 + wv * kWave + (uint32_t)j * 64u + lane < m) {
+      if ((uint32_t)j < J && r0 + wv * kWave + (uint32_t)j * 64u + lane < m) {
         const uint32_t o = base + wc[wv][k[j] & MASK] + lr[j];
         kout[o] = k[j];
         vout[o] = v[j];
