@@ -186,6 +186,9 @@ int klsh_comm_info(klsh_ctx* ctx, int* rank, int* world);
  *   "tail_big_screen"  1 (default) = there, 65..384-row runs are first screened on the fp16 image
  *                      in their workgroup; a run with no pair within the margin reads no f32 row
  *   "tail_screen_grid" workgroups of that screen's persistent launch (0 = 2048)
+ *   "hyperplane_async" 1 (default) = a call's hyperplanes are drawn on the host by a background
+ *                      thread while its first iterations run (uploaded as they are needed, no
+ *                      stream sync); 0 = drawn and uploaded before the loop starts
  *   "hip_events"       1 = HIP event pairs around the projection and the small-run merge of the
  *                      host-driven iterations (klsh_stats project_ms / small_ms, cross-checks of
  *                      the in-kernel stamps); 0 (default): none — a record costs ~9 us of stream

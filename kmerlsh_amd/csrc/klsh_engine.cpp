@@ -22,12 +22,14 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <cstring>
 #include <chrono>
 #include <cmath>
 #include <deque>
 #include <functional>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "klsh.h"
@@ -134,6 +136,17 @@ struct klsh_ctx {
   uint64_t w_k0 = 0, w_count = 0, w_cap = 0, w_alloc = 0;
   uint32_t w_base = 0;
   int w_dp = 0, w_d = 0;
+  // The call's window drawn in the background (predraw_hyperplanes): a host thread draws rows
+  // [w_k0, w_k0 + w_target) in order into pinned memory and publishes how many are done
+  // (w_drawn); ensure_hyperplanes uploads the drawn rows it needs on the stream, without a
+  // stream sync — the host RNG (~3.5 ms per C2 call, ~25 ms at C5's d = 512) runs beside the
+  // GPU's first iterations instead of in front of them.
+  std::thread drawer;
+  std::atomic<uint64_t> w_drawn{0};
+  std::atomic<bool> draw_stop{false};
+  uint64_t w_target = 0;
+  float* w_pin = nullptr;
+  size_t w_pin_floats = 0;
 
   // host
   std::vector<uint64_t> ids;  // member node -> k-mer id
@@ -227,6 +240,9 @@ struct klsh_ctx {
   }
   // "hyperplane_window" (klsh_set_option): rows drawn up front per call (0 = the default bound)
   uint64_t hyperplane_window = 0;
+  // "hyperplane_async" (klsh_set_option): 1 (default) = the call's window drawn by a background
+  // thread while the loop starts (predraw_hyperplanes); 0 = drawn and uploaded before it
+  uint32_t hyperplane_async = 1;
 
   int world() const { return comm ? comm->world : 1; }
   int rank() const { return comm ? comm->rank : 0; }
@@ -302,7 +318,19 @@ struct klsh_ctx {
     dfree(snap.nxt); dfree(snap.order);
     snap.valid = false;
   }
+  void join_drawer() {
+    if (drawer.joinable()) {
+      draw_stop.store(true);
+      drawer.join();
+      draw_stop.store(false);
+    }
+    w_target = 0;
+  }
   void release() {
+    join_drawer();
+    if (w_pin) (void)hipHostFree(w_pin);
+    w_pin = nullptr;
+    w_pin_floats = 0;
     release_shard();
     delete comm;
     comm = nullptr;
@@ -467,11 +495,29 @@ struct klsh_ctx {
 
   // Make hyperplanes [k0, k0+count) of stream `base` resident on the device (drawn on the host).
   // The resident window [w_k0, w_k0 + w_count) only grows forward; anything else restarts it.
+  // Rows [k0, k0 + count) inside the background-drawn window: true when ensure_hyperplanes can
+  // append them without touching rows the stream may be reading.
+  bool lazy_covers(uint32_t base, uint64_t k0, uint64_t count) const {
+    return w_target && W && w_base == base && w_dp == dp && w_d == d && k0 >= w_k0 &&
+           k0 + count <= w_k0 + w_target;
+  }
   int ensure_hyperplanes(uint32_t base, uint64_t k0, uint64_t count, double* host_ms) {
     if (count == 0) return 0;
     const bool same_stream = W && w_base == base && w_dp == dp && w_d == d;
     if (same_stream && k0 >= w_k0 && k0 + count <= w_k0 + w_count) return 0;
     const double t0 = now_ms();
+    if (lazy_covers(base, k0, count)) {  // wait for the drawer, then append what it has
+      const uint64_t need = k0 + count - w_k0;
+      while (w_drawn.load(std::memory_order_acquire) < need) std::this_thread::yield();
+      const uint64_t avail = w_drawn.load(std::memory_order_acquire);
+      KLSH_HIP(hipMemcpyAsync(W + w_count * dp, w_pin + w_count * dp,
+                              sizeof(float) * (avail - w_count) * dp, hipMemcpyHostToDevice,
+                              stream));
+      w_count = avail;
+      if (host_ms) *host_ms += now_ms() - t0;
+      return 0;
+    }
+    join_drawer();
     if (!(same_stream && k0 >= w_k0 && k0 + count <= w_k0 + w_cap)) {
       // (the window's row capacity carries over only for the same row width: w_cap rows of
       // another dp would scale the allocation by the width ratio on every change of d)
@@ -503,12 +549,63 @@ struct klsh_ctx {
   // (<= hmax) for all of them when that fits in 64 Mi floats (256 MB: C2 draws 11.5 K rows of 64),
   // else the first 64 iterations' worth — ensure_hyperplanes extends the window when the loop
   // gets there (-I 10000 at d = 4096 would otherwise need ~3.8 GB up front, host and device).
+  // The window is drawn by a background thread (see `drawer`) when it holds every iteration's rows;
+  // a smaller window (option hyperplane_window, or a call too long for 64 Mi floats) is drawn here
+  // and extended in place as before.
   int predraw_hyperplanes(uint32_t base, uint64_t k0, uint64_t hmax, int iterations,
                           double* host_ms) {
+    join_drawer();
     const uint64_t want = hmax * (uint64_t)iterations;
     const uint64_t cap = hyperplane_window ? hyperplane_window
                                            : std::max<uint64_t>(hmax * 64, (64ull << 20) / (uint64_t)dp);
-    return ensure_hyperplanes(base, k0, std::min(want, cap), host_ms);
+    const uint64_t count = std::min(want, cap);
+    if (count == 0) return 0;
+    if (hyperplane_window || count < want || !hyperplane_async)
+      return ensure_hyperplanes(base, k0, count, host_ms);
+    const double t0 = now_ms();
+    if (!w_pin || count * (uint64_t)dp > w_pin_floats) {
+      if (w_pin) (void)hipHostFree(w_pin);
+      w_pin = nullptr;
+      w_pin_floats = 0;
+      if (hipHostMalloc((void**)&w_pin, sizeof(float) * count * (uint64_t)dp,
+                        hipHostMallocDefault) != hipSuccess)
+        return fail(KLSH_E_HIP, "pinned hyperplane window");
+      w_pin_floats = count * (uint64_t)dp;
+    }
+    w_drawn.store(0);
+    float* out = w_pin;
+    const int dd = d, ddp = dp;
+    drawer = std::thread([this, base, k0, count, out, dd, ddp] {
+      // the first iterations' rows first (the loop starts on them), then larger chunks over the
+      // host's worker threads
+      uint64_t r = 0, chunk = 64;
+      while (r < count && !draw_stop.load(std::memory_order_relaxed)) {
+        const uint64_t n = std::min(chunk, count - r);
+        if (ddp != dd) std::memset(out + r * ddp, 0, sizeof(float) * n * ddp);  // row padding
+        klsh_host_hyperplanes(base, k0 + r, n, dd, ddp, out + r * ddp, chunk <= 64 ? 1 : 0);
+        r += n;
+        w_drawn.store(r, std::memory_order_release);
+        chunk = 2048;
+      }
+    });
+    // (the drawer runs meanwhile) a queued launch of an earlier call may still read the device
+    // window, which is rewritten from its first row
+    KLSH_HIP(hipStreamSynchronize(stream));
+    const uint64_t rows = std::max<uint64_t>(count, 4096);
+    if (!W || rows * (uint64_t)dp > w_alloc) {
+      dfree(W);
+      if (int e = dalloc(&W, rows * (uint64_t)dp)) return e;
+      w_alloc = rows * (uint64_t)dp;
+    }
+    w_cap = w_alloc / (uint64_t)dp;
+    w_k0 = k0;
+    w_count = 0;
+    w_base = base;
+    w_dp = dp;
+    w_d = d;
+    w_target = count;
+    if (host_ms) *host_ms += now_ms() - t0;
+    return 0;
   }
 
   // zero the iteration counters (and the run-list counters) on the stream
@@ -1101,7 +1198,8 @@ static int run_batched(klsh_ctx* ctx, float& threshold, float sim_step, int it, 
   const uint64_t need = (uint64_t)(it_end - it) * (uint64_t)h0;
   if (!(ctx->W && ctx->w_base == seed_base && ctx->w_dp == ctx->dp && ctx->w_d == ctx->d &&
         k0 >= ctx->w_k0 && k0 + need <= ctx->w_k0 + ctx->w_count)) {
-    KLSH_HIP(hipStreamSynchronize(s));  // a queued projection may still read the window
+    // a window restart may overwrite rows a queued projection still reads; an append may not
+    if (!ctx->lazy_covers(seed_base, k0, need)) KLSH_HIP(hipStreamSynchronize(s));
     if (int e = ctx->ensure_hyperplanes(seed_base, k0, need, &st->host_ms)) return e;
   }
   uint32_t* n_dev = ctx->n_next_dev;
@@ -1797,6 +1895,11 @@ int klsh_set_option(klsh_ctx* ctx, const char* name, int64_t value) {
   if (n == "tail_batch") return flag(&ctx->tail_batch);
   if (n == "huge_fold") return flag(&ctx->huge_fold_always);
   if (n == "tail_local") return flag(&ctx->tail_local);
+  if (n == "hyperplane_async") {
+    if (value != 0 && value != 1) return fail(KLSH_E_ARG, "hyperplane_async must be 0 or 1");
+    ctx->hyperplane_async = (uint32_t)value;
+    return 0;
+  }
   if (n == "hyperplane_window") {
     if (value < 0) return fail(KLSH_E_ARG, "hyperplane_window must be >= 0");
     ctx->hyperplane_window = (uint64_t)value;
@@ -1893,6 +1996,7 @@ int klsh_get_option(klsh_ctx* ctx, const char* name, int64_t* value) {
   else if (n == "huge_fold") *value = ctx->huge_fold_always;
   else if (n == "tail_local") *value = ctx->tail_local;
   else if (n == "hyperplane_window") *value = (int64_t)ctx->hyperplane_window;
+  else if (n == "hyperplane_async") *value = ctx->hyperplane_async;
   else if (n == "stop_after") *value = ctx->stop_after;
   else if (n == "progress") *value = ctx->progress;
   else if (n == "projection") *value = ctx->pw.variant;

@@ -773,6 +773,24 @@ def test_cluster_small_hyperplane_window_vs_oracle(engine, oracle, window):
     assert_same_result(engine.result(), o_rows, o_off, o_ids)
 
 
+@pytest.mark.parametrize("d,bthr,asy", [(13, 1000000, 1), (16, 2000, 1), (64, 1000000, 1),
+                                         (16, 2000, 0)])
+def test_cluster_hyperplane_async_vs_oracle(engine, oracle, d, bthr, asy):
+    """Option hyperplane_async (default 1): the call's hyperplanes drawn by a background host
+    thread while the first iterations run, uploaded as the loop needs them — d = 13 (padded rows
+    of the window), nested buckets (bthr = 2000: their draws run past the predrawn window and
+    fall back to the synchronous refill), twice in a row on one context (the drawer restarted)."""
+    rng = np.random.default_rng(d + bthr)
+    rows = clustered(rng, 30000, d, 400, 0.05)
+    want = oracle.cluster(rows, 0.8, 30, bthr, 41, 7)
+    with options(engine, hyperplane_async=asy):
+        for _ in range(2):
+            engine.load_rows(rows)
+            trace, counter, _ = engine.cluster(0.8, 30, bthr, 41, 7)
+            assert np.array_equal(trace, want[3]) and counter == want[4]
+            assert_same_result(engine.result(), *want[:3])
+
+
 def test_cluster_repeat_and_restore_deterministic(engine):
     rng = np.random.default_rng(5)
     rows = clustered(rng, 100000, 64, 2000, 0.05)

@@ -44,8 +44,14 @@ CLASSES = {
     "huge": r"k_merge_huge|k_merge_long",
     "compact": r"k_compact",
 }
-# the counter passes (collect_profiles.sh runs one FETCH_SIZE and one WRITE_SIZE pass each)
-PMC_CLASSES = ("project", "screen", "small", "sort", "tail", "runs", "compact")
+# the counter passes (collect_profiles.sh runs one FETCH_SIZE and one WRITE_SIZE pass each; the
+# merge classes, C4 and C5 through its "pmcx" passes)
+PMC_CLASSES = {
+    "c2": ("project", "screen", "small", "sort", "tail", "runs", "compact", "big128", "big192",
+           "big384", "big896"),
+    "c4": ("big384", "huge"),
+    "c5": ("project", "small", "big384"),
+}
 
 
 def one(pattern):
@@ -116,36 +122,44 @@ for cfg in ("c2", "c4", "c5"):
             shutil.copy(b, os.path.join(dst, f"{tag}_{cfg}_{kind}.log"))
 
 summary = {}
-for c in PMC_CLASSES:
-    rx = CLASSES[c]
-    vals = {}
-    for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        p = one(f"c2_{kind}_{c}/**/run_counter_collection.csv")
-        if not p:
-            continue
-        shutil.copy(p, os.path.join(dst, f"{tag}_c2_pmc_{kind}_{c}.csv"))
-        rows = [r for r in csv.DictReader(open(p)) if r["Counter_Name"] == counter]
-        start = loop_start(rows)
-        iters = sum(1 for r in rows if is_iter(r) and int(r["Dispatch_Id"]) >= start)
-        sel = [r for r in rows if int(r["Dispatch_Id"]) >= start and re.search(rx, r["Kernel_Name"])]
-        launches = len(sel) if len({r["Kernel_Name"] for r in sel}) == 1 else iters
-        vals[kind] = (sum(float(r["Counter_Value"]) for r in sel) * 1024.0, launches, len(sel),
-                      sorted({short(r["Kernel_Name"]) for r in sel}))
-    if "fetch" in vals and "write" in vals:
-        f, n, nd, names = vals["fetch"]
-        w = vals["write"][0]
-        summary.setdefault("c2", {})[c] = {
-            "kernels": names, "launches": n, "dispatches": nd,
-            "raw_fetch_bytes_per_launch": f / n, "raw_write_bytes_per_launch": w / n,
-            "hbm_bytes_per_launch": (2 * f + w) / n,
-            "correction": "FETCH_SIZE x2 (gfx950 counts 16-B/lane reads at half, "
-                          "MI355X_MICROARCH.md §HBM); WRITE_SIZE as read",
-            "note": "main-loop dispatches only; FETCH_SIZE counts Infinity-Cache hits too; the "
-                    "late iterations (<1M rows) are MALL-resident",
-            "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, "
-                      f"--kernel-include-regex '{rx}|k_project'), bench.py --steps 1 --warmup 0, "
-                      f"round {tag}",
-        }
+old_path = os.path.join(dst, "pmc_summary.json")
+if os.path.exists(old_path):  # classes not collected this time keep their earlier entries
+    summary = json.load(open(old_path))
+for cfg, classes in PMC_CLASSES.items():
+    for c in classes:
+        rx = CLASSES[c]
+        vals = {}
+        for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+            p = one(f"{cfg}_{kind}_{c}/**/run_counter_collection.csv")
+            if not p:
+                continue
+            shutil.copy(p, os.path.join(dst, f"{tag}_{cfg}_pmc_{kind}_{c}.csv"))
+            rows = [r for r in csv.DictReader(open(p)) if r["Counter_Name"] == counter]
+            start = loop_start(rows)
+            iters = sum(1 for r in rows if is_iter(r) and int(r["Dispatch_Id"]) >= start)
+            sel = [r for r in rows if int(r["Dispatch_Id"]) >= start and re.search(rx, r["Kernel_Name"])]
+            launches = len(sel) if len({r["Kernel_Name"] for r in sel}) == 1 else iters
+            vals[kind] = (sum(float(r["Counter_Value"]) for r in sel) * 1024.0, launches, len(sel),
+                          sorted({short(r["Kernel_Name"]) for r in sel}))
+        if "fetch" in vals and "write" in vals and vals["fetch"][1]:
+            f, n, nd, names = vals["fetch"]
+            w = vals["write"][0]
+            note = ("main-loop dispatches only; FETCH_SIZE counts Infinity-Cache hits too; the "
+                    "late iterations (<1M rows) are MALL-resident")
+            if cfg == "c5" and c == "big384":
+                note += ("; k_merge_big_wide<384,256,32> runs both the 129..192- and the "
+                         "193..384-row class (one dispatch each per iteration): their average")
+            summary.setdefault(cfg, {})[c] = {
+                "kernels": names, "launches": n, "dispatches": nd,
+                "raw_fetch_bytes_per_launch": f / n, "raw_write_bytes_per_launch": w / n,
+                "hbm_bytes_per_launch": (2 * f + w) / n,
+                "correction": "FETCH_SIZE x2 (gfx950 counts 16-B/lane reads at half, "
+                              "MI355X_MICROARCH.md §HBM); WRITE_SIZE as read",
+                "note": note,
+                "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, "
+                          f"--kernel-include-regex '{rx}|k_project'), bench.py --config {cfg} "
+                          f"--steps 1 --warmup 0, round {tag}",
+            }
 if summary:
     json.dump(summary, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
 print(json.dumps(summary, indent=1))
