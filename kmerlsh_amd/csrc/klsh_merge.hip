@@ -3952,19 +3952,13 @@ static void launch_groups(const Rows& r, uint32_t* slots, const Decider& dc, con
   const hipStream_t s_small = long_heavy ? f.lane(2) : s, s_long = long_heavy ? s : f.lane(2);
   // longest walks first on each stream; the longest runs (few, long walks) on the main stream,
   // concurrent with the auxiliary ones (it waits for them at the join)
-#ifndef KLSH_NT384
-#define KLSH_NT384 256
-#endif
-#ifndef KLSH_NT896
-#define KLSH_NT896 256
-#endif
-  launch_big<D, 384, KLSH_NT384, true>(w, 2, slots, dc, r, ctr, n, f.lane(0));
+  launch_big<D, 384, 256, true>(w, 2, slots, dc, r, ctr, n, f.lane(0));
   // many 385..896-row runs (w.big896_aux): they go on aux 2, ahead of the small runs, instead of
   // in front of the >896-row runs on the main stream — serialised, the two long-walk classes
   // make the main stream the critical path (C4 1794 -> 1432 ms); with a handful of them (C2)
   // the main stream is the better place (measured 281-285 vs 284-294 ms)
   if (!long896(w, dc, r))
-    launch_big<D, 896, KLSH_NT896, false>(w, 3, slots, dc, r, ctr, n, w.big896_aux ? f.lane(2) : s_long);
+    launch_big<D, 896, 256, false>(w, 3, slots, dc, r, ctr, n, w.big896_aux ? f.lane(2) : s_long);
   launch_huge(w, slots, dc, r, ctr, n, s_long);
   // 129..192 rows: two workgroups per CU (62 KB of LDS at d = 64, VGPRs capped at 256 like the
   // 65..128 class), ahead of 65..128 on aux 1
