@@ -38,6 +38,17 @@ struct RcclComm final : Comm {
   int wait_event(hipEvent_t e) override {
     return poll([&] { return hipEventQuery(e); });
   }
+  int wait_flag(const volatile uint32_t* flag, uint32_t want, hipStream_t s) override {
+    // the flag first; the stream (errors) and the communicator every 256 polls, as wait()
+    uint32_t spins = 0;
+    return poll([&] {
+      if ((int32_t)(*flag - want) >= 0) return hipSuccess;
+      if ((++spins & 63u) != 0) return hipErrorNotReady;  // (the stream only now and then)
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) return (int32_t)(*flag - want) >= 0 ? hipSuccess : hipErrorUnknown;
+      return q;
+    });
+  }
   template <class Query>
   int poll(Query query) {
     if (aborted) return check(ncclSuccess, "wait");

@@ -65,6 +65,25 @@ struct Comm {
     }
     return 0;
   }
+  // Wait until *flag (mapped host memory a kernel on stream s releases) reaches `want`; a stream
+  // error — or, RCCL, an asynchronous error or the timeout (as wait()) — ends it with -1.
+  virtual int wait_flag(const volatile uint32_t* flag, uint32_t want, hipStream_t s) {
+    for (uint64_t spins = 1; (int32_t)(*flag - want) < 0; ++spins) {
+      __builtin_ia32_pause();
+      if ((spins & 0xFFFu) == 0) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess && (int32_t)(*flag - want) < 0) {
+          err = "flag not released by a finished stream";
+          return -1;
+        }
+        if (q != hipSuccess && q != hipErrorNotReady) {
+          err = std::string("stream: ") + hipGetErrorString(q);
+          return -1;
+        }
+      }
+    }
+    return 0;
+  }
   double timeout_s = 600.0;  // option "comm_timeout_s"
   bool aborted = false;
   std::string err;

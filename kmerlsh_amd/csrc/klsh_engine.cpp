@@ -165,6 +165,11 @@ struct klsh_ctx {
   uint32_t* cntmat = nullptr;  // [W][W] pairs rank g sends rank r
   uint32_t* small = nullptr;   // [W + 1][4] per-rank counters exchange
   uint32_t* h_small = nullptr; // pinned: cntmat or the counters exchange
+  // mapped: the sharded loop's per-iteration publishes (k_publish_words): [sequence word, 64 B]
+  // [payload]; host and device views
+  uint32_t* shp_host = nullptr;
+  uint32_t* shp_dev = nullptr;
+  uint32_t shp_seq = 0;
   uint32_t* drec = nullptr;    // delta records of this rank, then of all ranks
   uint32_t* drec_all = nullptr;
   size_t drec_cap = 0, drec_all_cap = 0;  // words
@@ -252,6 +257,8 @@ struct klsh_ctx {
     dfree(owner); dfree(cntmat); dfree(small); dfree(drec); dfree(drec_all);
     if (h_small) (void)hipHostFree(h_small);
     h_small = nullptr;
+    if (shp_host) (void)hipHostFree(shp_host);
+    shp_host = shp_dev = nullptr;
     drec_cap = drec_all_cap = 0;
     shard_cap = 0;
   }
@@ -273,6 +280,21 @@ struct klsh_ctx {
                       hipHostMallocDefault) != hipSuccess) {
       release_shard();
       return fail(KLSH_E_NOMEM, "pinned exchange buffer");
+    }
+    {
+      const size_t words = 16 + std::max<size_t>((size_t)W * W, 4 * (size_t)W + sizeof(Counters) / 4);
+      void *hp = nullptr, *dp = nullptr;
+      if (hipHostMalloc(&hp, sizeof(uint32_t) * words, hipHostMallocMapped | hipHostMallocCoherent) !=
+              hipSuccess ||
+          hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+        if (hp) (void)hipHostFree(hp);
+        release_shard();
+        return fail(KLSH_E_NOMEM, "mapped exchange buffer");
+      }
+      memset(hp, 0, sizeof(uint32_t) * words);
+      shp_host = static_cast<uint32_t*>(hp);
+      shp_dev = static_cast<uint32_t*>(dp);
+      shp_seq = 0;
     }
     if (hipMemset(mark, 0, sizeof(uint32_t) * s) != hipSuccess) {
       release_shard();
@@ -1575,11 +1597,14 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
     // 1. keys of my rows, key-range ownership, send counts
     if (!ctx->ctr_clean) if (int e = ctx->reset_counters()) return e;
     ctx->ctr_clean = false;
-    KLSH_HIP(hipEventRecord(ctx->ev[0], s));
+    // (HIP events around the projection only with hip_events / phase_timing: a record is a
+    // marker packet the stream waits on, ~9 us per iteration)
+    const bool rec = ctx->hip_events || ctx->phase_timing;
+    if (rec) KLSH_HIP(hipEventRecord(ctx->ev[0], s));
     klsh::launch_project(ctx->rows, ctx->order, ctx->keys, n_g, ctx->hyperplane_ptr(k), h, 0u, s,
                          &ctx->pw);
     KLSH_HIP(hipGetLastError());
-    KLSH_HIP(hipEventRecord(ctx->ev[1], s));
+    if (rec) KLSH_HIP(hipEventRecord(ctx->ev[1], s));
     const int B = std::min(h, klsh::kMaxBinBits);
     const int shift = h - B;
     const uint32_t nbins = 1u << B;
@@ -1587,16 +1612,20 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
     if (timed_comm([&] { return cm->allgather(ctx->bins, ctx->bins_all, 4ull * nbins, s); }))
       return comm_fail("bin histogram allgather");
     klsh::launch_bin_split(ctx->bins_all, W, nbins, N, ctx->owner, ctx->cntmat, s);
-    KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->cntmat, 4ull * W * W, hipMemcpyDeviceToHost, s));
-    if (!ctx->counts_ev) KLSH_HIP(hipEventCreateWithFlags(&ctx->counts_ev, hipEventDisableTiming));
-    KLSH_HIP(hipEventRecord(ctx->counts_ev, s));
+    // the send counts to the host through mapped memory (k_publish_words): no copy, no event
+    const uint32_t seq_counts = ++ctx->shp_seq;
+    klsh::launch_publish_words(ctx->cntmat, (uint32_t)(W * W), nullptr, 0u, ctx->shp_dev + 16,
+                               ctx->shp_dev, seq_counts, s);
     // 2a. the stable partition by owner needs only the device's ownership map: it is queued
     //     before the host waits (for the counts only, not for it), so it runs during the round trip
     if (klsh::launch_partition(ctx->keys, ctx->order, n_g, shift, ctx->owner, W, ctx->nk1,
                                ctx->tile_sums, ctx->ctr, ctx->sbuf, s))
       return fail(KLSH_E_ARG, "partition: unsupported world size");
     KLSH_HIP(hipGetLastError());
-    if (timed_comm([&] { return cm->wait_event(ctx->counts_ev); })) return comm_fail("send counts");
+    if (timed_comm([&] { return cm->wait_flag(ctx->shp_host, seq_counts, s); }))
+      return comm_fail("send counts");
+    std::atomic_thread_fence(std::memory_order_acquire);
+    memcpy(ctx->h_small, ctx->shp_host + 16, 4ull * W * W);
     uint32_t m_g = 0;
     for (int r = 0; r < W; ++r) {
       scnt[r] = 8ull * ctx->h_small[g * W + r];
@@ -1635,9 +1664,16 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
     KLSH_HIP(hipMemcpyAsync(ctx->small + 4 * W, &ctx->ctr->n_over, 12, hipMemcpyDeviceToDevice, s));
     if (timed_comm([&] { return cm->allgather(ctx->small + 4 * W, ctx->small, 16, s); }))
       return comm_fail("counter allgather");
-    KLSH_HIP(hipMemcpyAsync(ctx->h_small, ctx->small, 16ull * W, hipMemcpyDeviceToHost, s));
-    KLSH_HIP(hipMemcpyAsync(ctx->h_ctr, ctx->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-    if (timed_comm([&] { return cm->wait(s); })) return comm_fail("counters");
+    // every rank's counters and this rank's Counters to the host through mapped memory
+    static_assert(sizeof(Counters) % 4 == 0, "Counters published as words");
+    const uint32_t seq_ctr = ++ctx->shp_seq;
+    klsh::launch_publish_words(ctx->small, (uint32_t)(4 * W), reinterpret_cast<const uint32_t*>(ctx->ctr),
+                               (uint32_t)(sizeof(Counters) / 4), ctx->shp_dev + 16, ctx->shp_dev,
+                               seq_ctr, s);
+    if (timed_comm([&] { return cm->wait_flag(ctx->shp_host, seq_ctr, s); })) return comm_fail("counters");
+    std::atomic_thread_fence(std::memory_order_acquire);
+    memcpy(ctx->h_small, ctx->shp_host + 16, 16ull * W);
+    memcpy(ctx->h_ctr, ctx->shp_host + 16 + 4 * W, sizeof(Counters));
     if (int e = ctx->check_device_err()) return e;
     if (ctx->phase_timing && st) {
       st->merge_ms += elapsed(ctx->ev[2], ctx->ev[3]);
@@ -1708,10 +1744,12 @@ static int cluster_sharded_body(klsh_ctx* ctx, float min_similarity, int iterati
 
     if (out == ctx->alt) std::swap(ctx->order, ctx->alt);
     const uint64_t N_next = std::accumulate(surv.begin(), surv.end(), (uint64_t)0);
-    st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
+    if (rec) {
+      st->project_ms += elapsed(ctx->ev[0], ctx->ev[1]);
+      st->project_timed_launches += 1;
+    }
     if (ctx->phase_timing) st->sort_ms += elapsed(ctx->ev[6], ctx->ev[5]);
     st->project_launches += 1;
-    st->project_timed_launches += 1;
     st->sum_rows += N;
     st->sum_proj_bits += N * (uint64_t)h;
     st->sum_merges += N - N_next;

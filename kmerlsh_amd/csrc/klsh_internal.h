@@ -362,6 +362,9 @@ void launch_compact(const uint32_t* slots, uint32_t n, uint32_t* out, uint32_t* 
                     const LookBack* lb = nullptr, const uint32_t* n_dev = nullptr);
 // Fold set `set` of blk into its totals and clear it (the end of a timed call).
 void launch_stamp_fold(KStampBlock* blk, int set, hipStream_t s);
+// a[0..na) then b[0..nb) to dst (mapped host memory, device view), then *seq_host = seq (release)
+void launch_publish_words(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb,
+                          uint32_t* dst, uint32_t* seq_host, uint32_t seq, hipStream_t s);
 
 // Mode-C producer: rows x[i] (slot i) from counts (d x bs, sample-major), LUT ln(c+1),
 // v_kmers; order[] = kept rows (sum > 0.1 d) compacted; ctr->total = kept count.

@@ -284,6 +284,27 @@ __global__ __launch_bounds__(256) void k_delta_apply(Rows r, const uint32_t* __r
   }
 }
 
+// The words the host needs from an exchange (send-count matrix; every rank's counters and this
+// rank's Counters) into mapped host memory, then the sequence word with a system-scope release:
+// the host polls it instead of a device-to-host copy plus an event or stream sync (two packets
+// and a wait each, ~10-20 us per exchange).  One workgroup.
+__global__ __launch_bounds__(256) void k_publish_words(const uint32_t* __restrict__ a, uint32_t na,
+                                                       const uint32_t* __restrict__ b, uint32_t nb,
+                                                       uint32_t* dst, uint32_t* seq_host,
+                                                       uint32_t seq) {
+  for (uint32_t i = threadIdx.x; i < na + nb; i += 256)
+    __hip_atomic_store(dst + i, i < na ? a[i] : b[i - na], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(seq_host, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_publish_words(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb,
+                          uint32_t* dst, uint32_t* seq_host, uint32_t seq, hipStream_t s) {
+  k_publish_words<<<1, 256, 0, s>>>(a, na, b, nb, dst, seq_host, seq);
+}
+
 void launch_delta_apply(const Rows& r, const uint32_t* rec, uint32_t n, hipStream_t s) {
   const uint64_t total = (uint64_t)n * (uint64_t)delta_words(r.dp);
   if (total)
