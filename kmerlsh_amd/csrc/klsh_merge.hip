@@ -944,6 +944,32 @@ __device__ __forceinline__ int run_class(uint32_t b, int bucket_thr) {
   return b >= 2 ? size_class(b) : -1;
 }
 
+// The entries of list l (0 <= l < kRunLists).  With a per-lane l this is a vector load from the
+// kernel-argument block, and a store through it waits for that load: the run-listing kernels read
+// the pointers once into an LDS table (run_list_table) instead of once per entry.
+__device__ __forceinline__ uint2* run_list_ptr(const MergeWork& w, int l) {
+  uint2* p = l == kRunLists - 2 ? w.huge : w.over;
+#pragma unroll
+  for (int c = 0; c < kBigClasses; ++c) p = l == kGroupClasses + c ? w.big[c] : p;
+#pragma unroll
+  for (int c = 0; c < kGroupClasses; ++c) p = l == c ? w.cls[c] : p;
+  return p;
+}
+
+// Threads 0 .. kRunLists-1 fill tab with the list pointers (visible after the next barrier),
+// typed as global memory: a generic pointer read back from LDS would make every entry store a
+// flat store, which the LDS waits that follow it also wait for.
+using RunListPtr = __attribute__((address_space(1))) uint64_t*;
+__device__ __forceinline__ void run_list_table(const MergeWork& w, RunListPtr* tab) {
+  const uint32_t t = threadIdx.x;
+  RunListPtr p = (RunListPtr)(uint64_t*)run_list_ptr(w, (int)min(t, (uint32_t)kRunLists - 1u));
+  if (t < (uint32_t)kRunLists) tab[t] = p;
+}
+// A (start, length) entry as one 64-bit store (uint2 layout: x in the low word).
+__device__ __forceinline__ uint64_t run_entry(uint32_t start, uint32_t len) {
+  return (uint64_t)len << 32 | start;
+}
+
 // What run counter `l` (kRunRows of them) receives for a run of b rows in list lr.
 __device__ __forceinline__ uint32_t run_contrib(int l, int lr, uint32_t b) {
   if (l < kRunLists) return l == lr ? 1u : 0u;
@@ -1168,9 +1194,18 @@ __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, uint32_t n, int
   __shared__ uint64_t hb[kRunTile / 64];
   __shared__ uint32_t lbase[kRunLists], lfill[kRunLists];
   __shared__ uint32_t s_tail_end;
+  __shared__ RunListPtr lptr[kRunLists];
   const uint32_t t = threadIdx.x;
   const uint32_t T0 = blockIdx.x * kRunTile;
-  if (t < kRunTile / 64) hb[t] = hbits[(size_t)blockIdx.x * (kRunTile / 64) + t];
+  // (the header loads unconditional, index clamped: issued together, one round trip)
+  uint32_t cb = 0u, te = 0u;
+  if constexpr (!SCAN) {
+    cb = counts[(size_t)min(t, (uint32_t)kRunLists - 1u) * ntiles + blockIdx.x];
+    te = tail_ends[blockIdx.x];
+  }
+  const uint64_t hv = hbits[(size_t)blockIdx.x * (kRunTile / 64) + (t & (kRunTile / 64 - 1u))];
+  run_list_table(w, lptr);
+  if (t < kRunTile / 64) hb[t] = hv;
   if constexpr (SCAN) {
     if (n_dev) n = *n_dev;
     __shared__ uint32_t red[2][4][kRunRows];
@@ -1208,10 +1243,10 @@ __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, uint32_t n, int
       *run_counter(w.rc, (int)t) = red[1][0][t] + red[1][1][t] + red[1][2][t] + red[1][3][t];
   } else {
     if (t < (uint32_t)kRunLists) {
-      lbase[t] = counts[(size_t)t * ntiles + blockIdx.x];
+      lbase[t] = cb;
       lfill[t] = 0u;
     }
-    if (t == 0) s_tail_end = tail_ends[blockIdx.x];
+    if (t == 0) s_tail_end = te;
   }
   __syncthreads();
   const uint32_t tail_end = s_tail_end;
@@ -1223,11 +1258,7 @@ __global__ __launch_bounds__(256) void k_runs_write(uint32_t lo, uint32_t n, int
       const int l = run_list(hb, T0, tail_end, q, bucket_thr, b);
       if (l < 0) continue;
       const uint32_t at = lbase[l] + atomicAdd(&lfill[l], 1u);
-      const uint2 e = make_uint2(lo + T0 + q, b);
-      if (l < kGroupClasses) w.cls[l][at] = e;
-      else if (l < kGroupClasses + kBigClasses) w.big[l - kGroupClasses][at] = e;
-      else if (l == kRunLists - 2) w.huge[at] = e;
-      else w.over[at] = e;
+      lptr[l][at] = run_entry(lo + T0 + q, b);
     }
   }
   kt_end(w.kt, KC_RUNS);
@@ -1259,6 +1290,7 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
   __shared__ uint32_t wc[4][kRad];    // per-wave digit counts of a round, then wave prefixes
   __shared__ uint32_t lcnt[kRunRows];  // this bucket's list counts, rows, heads
   __shared__ uint32_t lbase[kRunLists];
+  __shared__ RunListPtr lptr[kRunLists];
   __shared__ uint32_t red[4];
   kt_begin(w.kt, KC_RUNS);
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -1373,6 +1405,7 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     if (t < (uint32_t)kRunLists) lbase[t] = v;
   }
   if (t < (uint32_t)kRunLists) lcnt[t] = 0u;  // (reused as the list cursors)
+  run_list_table(w, lptr);
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < (int)kPer; ++q) {
@@ -1380,11 +1413,7 @@ __global__ __launch_bounds__(256) void k_tail_local(const uint32_t* __restrict__
     if (l >= 0) {
       const uint32_t dg = t * kPer + (uint32_t)q;
       const uint32_t at = lbase[l] + atomicAdd(&lcnt[l], 1u);
-      const uint2 e = make_uint2(base + cnt[dg], c4[q]);
-      if (l < kGroupClasses) w.cls[l][at] = e;
-      else if (l < kGroupClasses + kBigClasses) w.big[l - kGroupClasses][at] = e;
-      else if (l == kRunLists - 2) w.huge[at] = e;
-      else w.over[at] = e;
+      lptr[l][at] = run_entry(base + cnt[dg], c4[q]);
     }
   }
   // 3. the stable scatter, J * 256 keys per round (wave wv: positions wv*J*64 + j*64 + lane)
