@@ -2324,9 +2324,9 @@ __device__ __forceinline__ bool big_screen_pass(uint32_t b, const uint32_t* slot
         v[k] = *reinterpret_cast<const sh16x8*>(r.xh + (size_t)slot[a] * r.dp + sub);
       }
 #pragma unroll
-      for (int k = 0; k < KB; ++k) {
-        const uint32_t a = (g0 + (uint32_t)k) * RPR + rr;
-        if (a < b) *reinterpret_cast<sh16x8*>(hrows + a * STH + sub) = v[k];
+      for (int k = 0; k < KB; ++k) {  // (unconditional at the clamped index, as in big_runs)
+        const uint32_t a = min((g0 + (uint32_t)k) * RPR + rr, b - 1u);
+        *reinterpret_cast<sh16x8*>(hrows + a * STH + sub) = v[k];
       }
     }
   }
@@ -2494,10 +2494,14 @@ __device__ __forceinline__ void big_runs(const uint2* __restrict__ list, int cls
           const uint32_t a = min((g0 + (uint32_t)k) * RPR + rr, b - 1u);
           v[k] = *reinterpret_cast<const float4*>(r.x + (size_t)slot[a] * r.dp + sub);
         }
+        // (stores unconditional at the clamped index — a row past b rewrites row b - 1 with its own
+        // value: a store under `a < b` lets the compiler sink its load into the branch, and the KB
+        // loads become KB round trips.  A scheduling barrier between the two loops, to keep
+        // k_merge_tail's register-tight schedule from pairing the rest, spilled: not used)
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
-          const uint32_t a = (g0 + (uint32_t)k) * RPR + rr;
-          if (a < b) *reinterpret_cast<float4*>(rows + a * ST + sub) = v[k];
+          const uint32_t a = min((g0 + (uint32_t)k) * RPR + rr, b - 1u);
+          *reinterpret_cast<float4*>(rows + a * ST + sub) = v[k];
         }
       }
 #pragma unroll
