@@ -804,7 +804,10 @@ __global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X
   const uint32_t count = min(pw.ws[0], pw.cap);
   if (blockIdx.x * 256u < count) {
     // the h hyperplanes into LDS, 16 float4 loads in flight per lane (dp is a multiple of 4):
-    // a loop of one load per round trip was ~80 us of every launch, whatever its pair count
+    // a loop of one load per round trip was ~80 us of every launch, whatever its pair count.  The
+    // stores are unconditional at the clamped index (past nv - 1 they rewrite element nv - 1 with
+    // its own value): a store under `< nv` let the compiler sink each load into its branch, which
+    // made the 16 loads 16 round trips again
     const int nv = h * dp / 4;
     const float4* W4 = reinterpret_cast<const float4*>(W);
     float4* fw4 = reinterpret_cast<float4*>(fw);
@@ -814,8 +817,7 @@ __global__ __launch_bounds__(256) void k_project_fix(const float* __restrict__ X
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = W4[min(i0 + 256 * u, nv - 1)];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (i0 + 256 * u < nv) fw4[i0 + 256 * u] = v[u];
+      for (int u = 0; u < U; ++u) fw4[min(i0 + 256 * u, nv - 1)] = v[u];  // (see below)
     }
   }
   __syncthreads();

@@ -31,41 +31,75 @@ void launch_bin_hist(const uint32_t* keys, uint32_t n, int shift, uint32_t nbins
 
 // One workgroup of 256 lanes, 16 bins each.  A bin's owner is decided by the midpoint of its row
 // range in the global bin order, so ranges are contiguous and balanced to within one bin; every
-// rank computes the same.
+// rank computes the same.  A lane reads its 16 counts of a rank as four 16-B loads (nbins is a
+// power of two: at 16 bins or more a lane's bins are all in range and aligned) and adds a rank's
+// counts to the matrix once per owner run of its bins — no load waits on a branch over the value
+// of the one before (one lane-serial round trip per bin and rank: ≈ 16·W of them per iteration).
 __global__ __launch_bounds__(256) void k_bin_split(const uint32_t* __restrict__ hist_all,
                                                    int world, uint32_t nbins, uint64_t total,
                                                    uint32_t* __restrict__ owner,
                                                    uint32_t* __restrict__ cntmat) {
   constexpr uint32_t PER = (1u << kMaxBinBits) / 256;
+  static_assert(PER % 4 == 0, "whole 16-B loads");
   __shared__ uint32_t mat[kMaxRanks * kMaxRanks];
   for (uint32_t k = threadIdx.x; k < (uint32_t)(world * world); k += 256) mat[k] = 0;
   const uint32_t b0 = threadIdx.x * PER;
-  uint32_t tot[PER];
+  const uint32_t nb = b0 < nbins ? min(PER, nbins - b0) : 0u;  // this lane's bins
+  // rank r's counts of this lane's bins (0 past nb)
+  auto load = [&](int r, uint32_t (&c)[PER]) {
+    const uint32_t* src = hist_all + (size_t)r * nbins + b0;
+    if (nb == PER) {
+#pragma unroll
+      for (uint32_t q = 0; q < PER / 4; ++q) {
+        const uint4 v = reinterpret_cast<const uint4*>(src)[q];
+        c[4 * q] = v.x;
+        c[4 * q + 1] = v.y;
+        c[4 * q + 2] = v.z;
+        c[4 * q + 3] = v.w;
+      }
+    } else {  // fewer than 16 bins in all: lane 0 holds them
+#pragma unroll
+      for (uint32_t j = 0; j < PER; ++j) c[j] = j < nb ? src[j] : 0u;
+    }
+  };
+  uint32_t tot[PER] = {};
+#pragma unroll 2
+  for (int r = 0; r < world; ++r) {
+    uint32_t c[PER];
+    load(r, c);
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) tot[j] += c[j];
+  }
   uint32_t acc = 0;
 #pragma unroll
-  for (uint32_t j = 0; j < PER; ++j) {
-    uint32_t t = 0;
-    if (b0 + j < nbins)
-      for (int r = 0; r < world; ++r) t += hist_all[(size_t)r * nbins + b0 + j];
-    tot[j] = t;
-    acc += t;
-  }
+  for (uint32_t j = 0; j < PER; ++j) acc += tot[j];
   uint32_t block_total;
   uint64_t run = block_excl_scan_256(acc, &block_total);  // rows in bins before b0
+  uint32_t ow[PER];
 #pragma unroll
   for (uint32_t j = 0; j < PER; ++j) {
-    const uint32_t b = b0 + j;
-    if (b < nbins) {
-      const uint64_t mid2 = 2 * run + tot[j];  // twice the midpoint
-      const uint64_t o = total ? (mid2 * (uint64_t)world) / (2 * total) : 0;
-      const uint32_t ow = (uint32_t)(o >= (uint64_t)world ? world - 1 : o);
-      owner[b] = ow;
-      for (int g = 0; g < world; ++g) {
-        const uint32_t c = hist_all[(size_t)g * nbins + b];
-        if (c) atomicAdd(&mat[g * world + ow], c);
-      }
-    }
+    const uint64_t mid2 = 2 * run + tot[j];  // twice the midpoint
+    const uint64_t o = total ? (mid2 * (uint64_t)world) / (2 * total) : 0;
+    ow[j] = (uint32_t)(o >= (uint64_t)world ? world - 1 : o);
+    if (j < nb) owner[b0 + j] = ow[j];
     run += tot[j];
+  }
+  __syncthreads();  // (mat zeroed)
+#pragma unroll 2
+  for (int g = 0; g < world; ++g) {
+    uint32_t c[PER];
+    load(g, c);
+    uint32_t cur = ow[0], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+      if (j < nb && ow[j] != cur) {
+        if (sum) atomicAdd(&mat[g * world + cur], sum);
+        cur = ow[j];
+        sum = 0;
+      }
+      sum += c[j];
+    }
+    if (sum) atomicAdd(&mat[g * world + cur], sum);
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < (uint32_t)(world * world); k += 256) cntmat[k] = mat[k];
