@@ -3450,18 +3450,29 @@ __device__ __forceinline__ void stage_chunk(const float* __restrict__ X, int dp,
   const uint32_t lane = __lane_id();
   const uint32_t q = lane & (LPR - 1u), rsub = lane / LPR;
   const bool col_ok = (int)(4 * q) < kcp;
-  float4 v[LPR];
+  // Loads and stores unconditional (a lane past its run reads its slot's row, valid memory — the
+  // callers pass slot 0 there — and the column clamped to c0; both zeroed after the load): a
+  // load under `ok && col_ok` was a branch per row with its shuffles waited in front of it, and
+  // a store under `col_ok` lets the compiler sink the load into it.  Columns kcp .. KC of the
+  // tile (a partial last chunk) get zeros; the readers use n <= kcp of them.
+  uint32_t s[LPR];
+  bool ok[LPR];
 #pragma unroll
   for (int it = 0; it < LPR; ++it) {
     const uint32_t row = it * RPI + rsub;
-    const uint32_t s = shfl32(slot, row);
-    const int ok = __shfl(valid ? 1 : 0, (int)row, 64);
-    v[it] = (ok && col_ok) ? *reinterpret_cast<const float4*>(X + (size_t)s * dp + c0 + 4 * q)
-                           : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    s[it] = shfl32(slot, row);
+    const int vr = __shfl(valid ? 1 : 0, (int)row, 64);  // (every lane: a shuffle under col_ok
+    ok[it] = col_ok && vr != 0;                           // reads inactive lanes as 0)
   }
+  float4 v[LPR];
 #pragma unroll
   for (int it = 0; it < LPR; ++it)
-    if (col_ok) *reinterpret_cast<float4*>(tile + (it * RPI + rsub) * ST + 4 * q) = v[it];
+    v[it] = *reinterpret_cast<const float4*>(X + (size_t)s[it] * dp + c0 + (col_ok ? 4 * q : 0u));
+#pragma unroll
+  for (int it = 0; it < LPR; ++it) {
+    if (!ok[it]) v[it] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    *reinterpret_cast<float4*>(tile + (it * RPI + rsub) * ST + 4 * q) = v[it];
+  }
 }
 
 template <int N>
