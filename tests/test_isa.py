@@ -14,7 +14,8 @@ import pytest
 from conftest import ROOT
 
 CSRC = os.path.join(ROOT, "kmerlsh_amd", "csrc")
-ASMS = [os.path.join(ROOT, "kmerlsh_amd", "build", f) for f in ("klsh_kernels.s", "klsh_merge.s")]
+ASMS = [os.path.join(ROOT, "kmerlsh_amd", "build", f)
+        for f in ("klsh_kernels.s", "klsh_merge.s", "klsh_shard.s")]
 FMA = re.compile(r"^\s+(v_fma\w*|v_fmac\w*|v_pk_fma\w*|v_mad_f32\w*|v_fmamk\w*|v_fmaak\w*)\b")
 
 
@@ -78,3 +79,53 @@ def test_correctly_rounded_division_and_sqrt(kernels):
     body = kernels[next(k for k in kernels if "k_fp_selftest" in k)]
     assert "v_div_scale_f32" in body and "v_div_fixup_f32" in body
     assert "v_sqrt_f32" in body
+
+
+def _ops(body):
+    """The instruction lines of a kernel body (labels, comments and directives dropped)."""
+    out = []
+    for ln in body.splitlines():
+        t = ln.strip()
+        if t and not t.startswith((";", ".")) and not t.endswith(":"):
+            out.append(t)
+    return out
+
+
+def _waited_loads(body, load=r"(global|buffer|flat)_load\w*"):
+    """Vector loads followed at once by s_waitcnt vmcnt(0): each one a round trip of its own."""
+    ops = _ops(body)
+    pat = re.compile(load)
+    return [ops[i] for i in range(len(ops) - 1)
+            if pat.match(ops[i]) and ops[i + 1].startswith("s_waitcnt") and "vmcnt(0)" in ops[i + 1]]
+
+
+def _kernel(kernels, *parts):
+    names = [k for k in kernels if all(p in k for p in parts)]
+    assert names, parts
+    return names
+
+
+def test_load_batches_stay_in_flight(kernels):
+    """Regression guard for the load->wait chains the round-6 ISA audit removed:
+    a per-lane index into a kernel-argument pointer array, a store under a bounds branch that lets
+    the compiler sink its load into the branch, a load then a branch on its value."""
+    # run listing: no pointer load per entry, no flat (generic) entry stores
+    for name in _kernel(kernels, "k_tail_local") + _kernel(kernels, "k_runs_write"):
+        body = kernels[name]
+        assert not any(op.startswith("flat_") for op in _ops(body)), name
+        # (one: the list-pointer table itself, read once per workgroup)
+        assert len(_waited_loads(body, r"global_load_dwordx2")) <= 1, (name, _waited_loads(body)[:4])
+    # big-run row staging (LDS rows at d = 16 / 32 / 64): no load -> wait -> LDS store triples
+    for name in [k for k in kernels if "k_merge_bigIL" in k and "ELb1E" in k]:
+        ops = _ops(kernels[name])
+        triples = [i for i in range(len(ops) - 2)
+                   if ops[i].startswith("global_load_dwordx4") and "vmcnt(0)" in ops[i + 1]
+                   and ops[i + 2].startswith("ds_write_b128")]
+        assert not triples, (name, len(triples))
+    # k_project_fix's hyperplane staging and the wide group merges' chunk staging
+    for name in _kernel(kernels, "k_project_fix") + _kernel(kernels, "k_merge_group_wide"):
+        w = _waited_loads(kernels[name], r"global_load_dwordx4")
+        assert len(w) <= 1, (name, len(w))
+    # the sharded loop's bin split
+    for name in _kernel(kernels, "k_bin_split"):
+        assert len(_waited_loads(kernels[name])) <= 2, name
