@@ -3020,6 +3020,22 @@ __device__ __noinline__ uint32_t long_rescan(const uint64_t* Py, uint32_t lo, ui
 // One position of k_merge_long past the register ones: its row from memory against the new row
 // (short chains + pre-screen, the sequential chains for a close call); the row copied to `last`
 // if given.  Out of line: the register positions' rows stay live around the call.
+// dst[0, D) = src[0, D) for a global row src and an LDS row dst, typed as such: through the
+// generic pointers every element was a flat load waited for before its flat store.
+template <int D>
+__device__ __forceinline__ void copy_row_to_lds(float* dst, const float* src) {
+  typedef float f4 __attribute__((ext_vector_type(4)));  // (a builtin vector: assignable there)
+  using G4 = const __attribute__((address_space(1))) f4*;
+  using L4 = __attribute__((address_space(3))) f4*;
+  const G4 g = (G4)(const f4*)src;
+  const L4 l = (L4)(f4*)dst;
+  f4 v[D / 4];
+#pragma unroll
+  for (int k = 0; k < D / 4; ++k) v[k] = g[k];
+#pragma unroll
+  for (int k = 0; k < D / 4; ++k) l[k] = v[k];
+}
+
 template <int D>
 __device__ __noinline__ uint32_t long_mem_decide(const float* xp, const float* cw, float sy,
                                                  float sc_a, Decider dc, float* last) {
@@ -3040,11 +3056,10 @@ __device__ __noinline__ uint32_t long_mem_decide(const float* xp, const float* c
     for (int k = 0; k < D; ++k) dot = dot + xp[k] * cw[k];
     v = decide(dc, dot, sy * __builtin_sqrtf(nn)) ? 1u : 0u;
   }
-  // (the copy below is one round trip per element — the pointers may alias — but it runs for
-  // one position per step; the row kept in registers for it instead measured slower: C4 892 ->
-  // 907 ms, the extra registers of this out-of-line call saved and restored around it)
-  if (last)
-    for (int k = 0; k < D; ++k) last[k] = xp[k];
+  // (the row kept in registers from the loop above for this copy measured slower: C4 892 ->
+  // 907 ms, the extra registers of this out-of-line call saved and restored around it; an
+  // element loop here was one round trip per element — the pointers may alias)
+  if (last) copy_row_to_lds<D>(last, xp);  // (last: the caller's LDS row)
   return v;
 }
 

@@ -126,6 +126,9 @@ def test_load_batches_stay_in_flight(kernels):
     for name in _kernel(kernels, "k_project_fix") + _kernel(kernels, "k_merge_group_wide"):
         w = _waited_loads(kernels[name], r"global_load_dwordx4")
         assert len(w) <= 1, (name, len(w))
+    # k_merge_long's row copy for the next step (global -> LDS, typed: not a flat chain)
+    for name in _kernel(kernels, "long_mem_decide"):
+        assert len(_waited_loads(kernels[name])) <= 2, name
     # the sharded loop's bin split
     for name in _kernel(kernels, "k_bin_split"):
         assert len(_waited_loads(kernels[name])) <= 2, name
