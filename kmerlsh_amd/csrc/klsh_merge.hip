@@ -3017,33 +3017,39 @@ __device__ __noinline__ uint32_t long_rescan(const uint64_t* Py, uint32_t lo, ui
   return 0xFFFFFFFFu;
 }
 
-// One position of k_merge_long past the register ones: its row from memory against the new row
-// (short chains + pre-screen, the sequential chains for a close call); the row copied to `last`
-// if given.  Out of line: the register positions' rows stay live around the call.
-// dst[0, D) = src[0, D) for a global row src and an LDS row dst, typed as such: through the
-// generic pointers every element was a flat load waited for before its flat store.
+// Typed views of a global row and an LDS row as 16-B vectors (builtin vectors: assignable in an
+// address space).  Through generic pointers every access is a flat one (both wait counters, and
+// a flat load-store pair per element where the compiler cannot rule out overlap).
+typedef float klsh_f4 __attribute__((ext_vector_type(4)));
+using GRow4 = const __attribute__((address_space(1))) klsh_f4*;
+using LRow4 = __attribute__((address_space(3))) klsh_f4*;
+
+// dst[0, D) = src[0, D) for a global row src and an LDS row dst: every load before the stores.
 template <int D>
 __device__ __forceinline__ void copy_row_to_lds(float* dst, const float* src) {
-  typedef float f4 __attribute__((ext_vector_type(4)));  // (a builtin vector: assignable there)
-  using G4 = const __attribute__((address_space(1))) f4*;
-  using L4 = __attribute__((address_space(3))) f4*;
-  const G4 g = (G4)(const f4*)src;
-  const L4 l = (L4)(f4*)dst;
-  f4 v[D / 4];
+  const GRow4 g = (GRow4)(const klsh_f4*)src;
+  const LRow4 l = (LRow4)(klsh_f4*)dst;
+  klsh_f4 v[D / 4];
 #pragma unroll
   for (int k = 0; k < D / 4; ++k) v[k] = g[k];
 #pragma unroll
   for (int k = 0; k < D / 4; ++k) l[k] = v[k];
 }
 
+// One position of k_merge_long past the register ones: its row from memory against the new row
+// (short chains + pre-screen, the sequential chains for a close call); the row copied to `last`
+// if given.  Out of line: the register positions' rows stay live around the call.  xp: a global
+// row; cw, last: LDS rows (typed below).
 template <int D>
 __device__ __noinline__ uint32_t long_mem_decide(const float* xp, const float* cw, float sy,
                                                  float sc_a, Decider dc, float* last) {
+  const GRow4 xg = (GRow4)(const klsh_f4*)xp;
+  const LRow4 cl = (LRow4)(klsh_f4*)const_cast<float*>(cw);
   float d4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int k = 0; k < D; k += 4) {
-    const float4 u = *reinterpret_cast<const float4*>(cw + k);
-    const float4 xv = *reinterpret_cast<const float4*>(xp + k);
+    const klsh_f4 u = cl[k / 4];
+    const klsh_f4 xv = xg[k / 4];
     d4[0] = d4[0] + xv.x * u.x;
     d4[1] = d4[1] + xv.y * u.y;
     d4[2] = d4[2] + xv.z * u.z;
